@@ -1,0 +1,246 @@
+"""Generate the golden fixtures under tests/golden/ by RUNNING the reference.
+
+Runs ONLY in the build container (the reference at /root/reference never travels to
+the GPU box).  Output: small .npz files, data only (inputs, masks, outputs, grad and
+parameter checksums).  Re-run with:
+
+    python tests/golden/make_golden.py
+
+Accommodations needed to import the reference here:
+  * `timm` is not installed.  The reference uses only `timm.layers.DropPath` and
+    `timm.layers.trunc_normal_` (tiny_vit.py:5, mae_vit_adapter.py:3).  A module
+    `timm.layers` is injected with timm's published algorithms (stochastic depth
+    with scale_by_keep; trunc_normal_ = torch.nn.init.trunc_normal_).  Both only
+    matter for init (overwritten below) and DropPath (forced to p=0 for parity).
+  * `torchvision` / `tensorboard` are not installed; train_ssl_mae.py imports them
+    at module scope (:10-11) but `train_one_epoch`/`patchify` never touch them, so
+    empty placeholder modules are injected.
+  * HF `datasets` shadows `src/datasets`, so mae_loader.py is loaded by file path.
+
+Parity mode: every Dropout p=0, MultiheadAttention.dropout=0, DropPath p=0; BN in
+train mode (batch statistics); gradient checkpointing ON as shipped.
+"""
+import importlib.util
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF_SRC = "/root/reference/src"
+sys.path.insert(0, os.path.join(REPO, "ssl-vit-video-analytics_amd"))
+from ssl_mae_amd.init_rule import apply_rule, synthetic_clip  # noqa: E402
+
+
+def _install_stubs():
+    timm = types.ModuleType("timm")
+    layers = types.ModuleType("timm.layers")
+
+    def drop_path(x, drop_prob=0.0, training=False, scale_by_keep=True):
+        if drop_prob == 0.0 or not training:
+            return x
+        keep = 1 - drop_prob
+        shape = (x.shape[0],) + (1,) * (x.ndim - 1)
+        r = x.new_empty(shape).bernoulli_(keep)
+        if keep > 0.0 and scale_by_keep:
+            r.div_(keep)
+        return x * r
+
+    class DropPath(torch.nn.Module):
+        def __init__(self, drop_prob=0.0, scale_by_keep=True):
+            super().__init__()
+            self.drop_prob = drop_prob
+            self.scale_by_keep = scale_by_keep
+
+        def forward(self, x):
+            return drop_path(x, self.drop_prob, self.training, self.scale_by_keep)
+
+    def trunc_normal_(tensor, mean=0.0, std=1.0, a=-2.0, b=2.0):
+        return torch.nn.init.trunc_normal_(tensor, mean, std, a, b)
+
+    layers.DropPath = DropPath
+    layers.trunc_normal_ = trunc_normal_
+    timm.layers = layers
+    sys.modules["timm"] = timm
+    sys.modules["timm.layers"] = layers
+
+    tb = types.ModuleType("torch.utils.tensorboard")
+    tb.SummaryWriter = object
+    sys.modules["torch.utils.tensorboard"] = tb
+    tv = types.ModuleType("torchvision")
+    tvt = types.ModuleType("torchvision.transforms")
+    tv.transforms = tvt
+    sys.modules["torchvision"] = tv
+    sys.modules["torchvision.transforms"] = tvt
+
+
+def _import_reference():
+    _install_stubs()
+    sys.path.insert(0, REF_SRC)
+    spec = importlib.util.spec_from_file_location(
+        "ref_mae_loader", os.path.join(REF_SRC, "datasets", "mae_loader.py"))
+    mae_loader = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mae_loader)
+    # train_ssl_mae does `from datasets.mae_loader import ...`: route it to the file.
+    pkg = types.ModuleType("datasets")
+    pkg.mae_loader = mae_loader
+    saved = {k: sys.modules.get(k) for k in ("datasets", "datasets.mae_loader")}
+    sys.modules["datasets"] = pkg
+    sys.modules["datasets.mae_loader"] = mae_loader
+    import models.tiny_vit as tiny_vit
+    import models.mae_vit_adapter as adapter
+    import utils as ref_utils
+    import train_ssl_mae
+    for k, v in saved.items():
+        if v is None:
+            sys.modules.pop(k, None)
+        else:
+            sys.modules[k] = v
+    return tiny_vit, adapter, mae_loader, ref_utils, train_ssl_mae
+
+
+def _parity_mode(model):
+    for m in model.modules():
+        if isinstance(m, torch.nn.Dropout):
+            m.p = 0.0
+        if isinstance(m, torch.nn.MultiheadAttention):
+            m.dropout = 0.0
+        if hasattr(m, "drop_prob"):
+            m.drop_prob = 0.0
+
+
+class _Logger:
+    def info(self, *a, **k):
+        pass
+
+
+class _Writer:
+    def add_scalar(self, *a, **k):
+        pass
+
+
+def make_config(T, S, ratio, depth=4, dim=384, heads=6, batch=2):
+    return {
+        "dataset": {"clip_len": T, "image_size": S, "stride": 4, "train_split": "-"},
+        "model": {"decoder_embed_dim": dim, "decoder_depth": depth, "decoder_num_heads": heads},
+        "ssl": {"mask_ratio": ratio, "norm_pix_loss": True},
+        "training": {"batch_size": batch, "lr": 5e-4, "log_interval": 20},
+    }
+
+
+def run_case(ref, name, B, T, S, ratio, steps, record_acts=True, clip_seed=1234):
+    tiny_vit, adapter, mae_loader, ref_utils, tr = ref
+    torch.set_num_threads(8)
+    cfg = make_config(T, S, ratio, batch=B)
+    encoder = tiny_vit.tiny_vit_21m_variant(img_size=S, use_checkpoint=True)
+    model = adapter.TinyVideoMAE(encoder, cfg)
+    apply_rule(model)
+    _parity_mode(model)
+    clips = [torch.from_numpy(synthetic_clip(B, T, S, seed=clip_seed + i)) for i in range(steps)]
+
+    rec = {}
+    acts = {}
+    masks = []
+    orig_mask_fn = tr.get_tube_mask
+
+    def mask_spy(*a):
+        m = orig_mask_fn(*a)
+        masks.append(m.clone())
+        return m
+    tr.get_tube_mask = mask_spy
+
+    hooks = []
+    if record_acts:
+        def grab(key):
+            def h(mod, inp, out):
+                if key not in acts:
+                    acts[key] = out.detach().clone()
+            return h
+        hooks.append(model.encoder.patch_embed.register_forward_hook(grab("act_stem")))
+        for i in range(3):
+            hooks.append(model.encoder.stages[i].register_forward_hook(grab(f"act_stage{i}")))
+        hooks.append(model.register_forward_hook(grab("pred")))
+
+    optimizer = torch.optim.AdamW(model.parameters(), lr=5e-4, weight_decay=0.05)
+    scaler = torch.amp.GradScaler("cuda")
+    ref_utils.set_seed(42)
+    avg_loss, _ = tr.train_one_epoch(model, clips, optimizer, scaler, 1, torch.device("cpu"),
+                                     cfg, _Writer(), _Logger())
+    tr.get_tube_mask = orig_mask_fn
+    for h in hooks:
+        h.remove()
+
+    rec["B"], rec["T"], rec["S"], rec["ratio"], rec["steps"] = B, T, S, ratio, steps
+    rec["clip_seed"] = clip_seed
+    rec["avg_loss"] = np.float64(avg_loss)
+    rec["mask"] = torch.stack(masks).numpy()
+    if B * T * S * S <= 64 * 64 * 8:
+        rec["clip"] = clips[0].numpy()
+    for k, v in acts.items():
+        a = v.float().numpy()
+        if a.size <= 300_000:
+            rec[k] = a
+        rec[k + "_sum"] = np.float64(a.astype(np.float64).sum())
+        rec[k + "_sumsq"] = np.float64((a.astype(np.float64) ** 2).sum())
+    if steps == 1:
+        with torch.no_grad():
+            tgt = tr.patchify(clips[0], p=8)
+            rec["target_raw_rows"] = tgt[0, :4].numpy()
+    for n, p in model.named_parameters():
+        pv = p.detach().double().numpy().ravel()
+        rec["param_sum/" + n] = np.float64(pv.sum())
+        rec["param_head/" + n] = pv[:8].astype(np.float32)
+        if p.grad is not None:
+            g = p.grad.detach().double().numpy().ravel()
+            rec["grad_sum/" + n] = np.float64(g.sum())
+            rec["grad_sumsq/" + n] = np.float64((g * g).sum())
+            rec["grad_head/" + n] = g[:8].astype(np.float32)
+    for n, b in model.named_buffers():
+        rec["buf/" + n] = b.detach().numpy().copy()
+    out = os.path.join(HERE, f"{name}.npz")
+    np.savez_compressed(out, **rec)
+    print(f"wrote {out}: avg_loss={avg_loss:.6f} keys={len(rec)}")
+
+
+def masks_case(ref):
+    _, _, mae_loader, ref_utils, _ = ref
+    rec = {}
+    for (B, T, L, r) in [(4, 8, 784, 0.75), (40, 16, 196, 0.9), (256, 8, 784, 0.75),
+                         (3, 2, 16, 0.0), (3, 2, 16, 1.0), (2, 1, 1, 0.75), (5, 3, 7, 0.5)]:
+        ref_utils.set_seed(42)
+        m = mae_loader.get_tube_mask(B, T, L, r)
+        rec[f"mask_{B}_{T}_{L}_{r}"] = m.numpy()
+    # two consecutive draws from one seeding (the RNG stream continues)
+    ref_utils.set_seed(42)
+    a = mae_loader.get_tube_mask(4, 8, 784, 0.75)
+    b = mae_loader.get_tube_mask(4, 8, 784, 0.75)
+    rec["mask_seq_a"] = a.numpy()
+    rec["mask_seq_b"] = b.numpy()
+    out = os.path.join(HERE, "tube_masks.npz")
+    np.savez_compressed(out, **rec)
+    print("wrote", out)
+
+
+def patchify_case(ref):
+    tr = ref[4]
+    rec = {}
+    x = torch.arange(2 * 3 * 2 * 16 * 24, dtype=torch.float32).reshape(2, 3, 2, 16, 24)
+    rec["patchify_in_shape"] = np.array(x.shape)
+    rec["patchify_out"] = tr.patchify(x, p=8).numpy()
+    out = os.path.join(HERE, "patchify.npz")
+    np.savez_compressed(out, **rec)
+    print("wrote", out)
+
+
+if __name__ == "__main__":
+    ref = _import_reference()
+    masks_case(ref)
+    patchify_case(ref)
+    run_case(ref, "step_b2_t2_s32", B=2, T=2, S=32, ratio=0.75, steps=1)
+    run_case(ref, "step2_b2_t2_s32", B=2, T=2, S=32, ratio=0.75, steps=2)
+    run_case(ref, "step_b2_t4_s64", B=2, T=4, S=64, ratio=0.9, steps=1)
+    if "--full" in sys.argv:
+        run_case(ref, "step_b1_t8_s224", B=1, T=8, S=224, ratio=0.75, steps=1)

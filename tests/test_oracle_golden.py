@@ -1,0 +1,134 @@
+"""Pin the CPU oracle (oracle/mae_oracle.py) against fixtures produced by running the
+reference itself (tests/golden/make_golden.py).  CPU only."""
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import mae_oracle as O
+from ssl_mae_amd.init_rule import param_value, synthetic_clip
+
+STEP_CASES = ["step_b2_t2_s32", "step_b2_t4_s64", "step_b1_t8_s224"]
+
+
+def _cfg(d):
+    return {"dataset": {"clip_len": int(d["T"]), "image_size": int(d["S"])},
+            "model": {"decoder_embed_dim": 384, "decoder_depth": 4, "decoder_num_heads": 6},
+            "ssl": {"mask_ratio": float(d["ratio"]), "norm_pix_loss": True}}
+
+
+def _close(a, b, rtol, atol):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    err = np.abs(a - b) - (atol + rtol * np.abs(b))
+    return float(err.max()) <= 0.0, float(np.abs(a - b).max())
+
+
+def test_tube_masks_bit_exact(golden_dir):
+    d = np.load(os.path.join(golden_dir, "tube_masks.npz"))
+    for k in d.files:
+        if not k.startswith("mask_") or k.startswith("mask_seq"):
+            continue
+        _, B, T, L, r = k.split("_")
+        torch.manual_seed(42)
+        m = O.get_tube_mask(int(B), int(T), int(L), float(r))
+        assert m.dtype == torch.bool
+        assert np.array_equal(m.numpy(), d[k]), k
+    torch.manual_seed(42)
+    a = O.get_tube_mask(4, 8, 784, 0.75)
+    b = O.get_tube_mask(4, 8, 784, 0.75)
+    assert np.array_equal(a.numpy(), d["mask_seq_a"])
+    assert np.array_equal(b.numpy(), d["mask_seq_b"])
+
+
+def test_patchify_golden(golden_dir):
+    d = np.load(os.path.join(golden_dir, "patchify.npz"))
+    shape = tuple(int(s) for s in d["patchify_in_shape"])
+    x = torch.arange(int(np.prod(shape)), dtype=torch.float32).reshape(shape)
+    assert np.array_equal(O.patchify(x, 8).numpy(), d["patchify_out"])
+
+
+@pytest.mark.parametrize("case", STEP_CASES)
+def test_train_step_matches_reference(golden_dir, case):
+    path = os.path.join(golden_dir, case + ".npz")
+    if not os.path.exists(path):
+        pytest.skip("fixture not generated")
+    d = np.load(path)
+    cfg = _cfg(d)
+    B, T, S = int(d["B"]), int(d["T"]), int(d["S"])
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    P = O.make_params(cfg, param_value)
+    bufs = O.init_buffers(P)
+    opt = O.AdamWState(lr=5e-4)
+    clip = torch.from_numpy(synthetic_clip(B, T, S, seed=int(d["clip_seed"])))
+    if "clip" in d.files:
+        assert np.array_equal(clip.numpy(), d["clip"])
+    # the mask the reference drew inside train_one_epoch after set_seed(42)
+    torch.manual_seed(42)
+    L = (S // 8) ** 2
+    mask = O.get_tube_mask(B, T, L, float(d["ratio"]))
+    assert np.array_equal(mask.numpy(), d["mask"][0])
+    acts = {}
+    loss, grads = O.train_step(P, bufs, opt, clip, mask, cfg, acts)
+    assert abs(loss.item() - float(d["avg_loss"])) < 1e-5 * max(1.0, abs(float(d["avg_loss"])))
+    for k in ("act_stem", "act_stage0", "act_stage1", "act_stage2", "pred"):
+        a = acts[k].detach().double()
+        ok, e = _close(a.sum().item(), d[k + "_sum"], 1e-4,
+                       1e-5 * math.sqrt(float(d[k + "_sumsq"]) * a.numel()))
+        assert ok, (k, e)
+        ok, e = _close((a * a).sum().item(), d[k + "_sumsq"], 1e-4, 0)
+        assert ok, (k, "sumsq", e)
+        if k in d.files:
+            ok, e = _close(a.numpy(), d[k], 1e-4, 1e-4)
+            assert ok, (k, "full", e)
+    n_grads = 0
+    for name, g in grads.items():
+        key = "grad_sum/" + name
+        if key not in d.files:
+            assert g is None, name
+            continue
+        n_grads += 1
+        g = g.double()
+        scale = math.sqrt(float(d["grad_sumsq/" + name]))
+        ok, e = _close((g * g).sum().item(), d["grad_sumsq/" + name], 2e-4, 1e-12)
+        assert ok, (name, "sumsq", e)
+        ok, e = _close(g.sum().item(), d[key], 1e-3, 1e-5 * scale * math.sqrt(g.numel()) + 1e-6)
+        assert ok, (name, "sum", e)
+        ok, e = _close(g.reshape(-1)[:8].numpy(), d["grad_head/" + name], 1e-3, 1e-5 * scale + 1e-7)
+        assert ok, (name, "head", e)
+    assert n_grads == len([k for k in d.files if k.startswith("grad_sum/")])
+    for name, p in P.items():
+        # Adam turns a pure-rounding-noise gradient (|g| ~ 1e-9, e.g. the bias of a BN
+        # feeding another batch-stat BN) into a +-lr step of arbitrary sign.
+        gh = d["grad_head/" + name] if ("grad_head/" + name) in d.files else np.zeros(8)
+        atol = np.where(np.abs(gh[: p.numel()]) < 1e-6, 2.1 * 5e-4, 1e-6)
+        ok, e = _close(p.reshape(-1)[:8].numpy(), d["param_head/" + name], 1e-5, atol)
+        assert ok, (name, "param", e)
+    for name, b in bufs.items():
+        ok, e = _close(b.numpy(), d["buf/" + name], 1e-4, 1e-5)
+        assert ok, (name, "buf", e)
+
+
+def test_two_steps_match_reference(golden_dir):
+    d = np.load(os.path.join(golden_dir, "step2_b2_t2_s32.npz"))
+    cfg = _cfg(d)
+    B, T, S = int(d["B"]), int(d["T"]), int(d["S"])
+    P = O.make_params(cfg, param_value)
+    bufs = O.init_buffers(P)
+    opt = O.AdamWState(lr=5e-4)
+    torch.manual_seed(42)
+    losses = []
+    for i in range(2):
+        clip = torch.from_numpy(synthetic_clip(B, T, S, seed=int(d["clip_seed"]) + i))
+        mask = O.get_tube_mask(B, T, (S // 8) ** 2, float(d["ratio"]))
+        assert np.array_equal(mask.numpy(), d["mask"][i])
+        loss, _ = O.train_step(P, bufs, opt, clip, mask, cfg)
+        losses.append(loss.item())
+    assert abs(np.mean(losses) - float(d["avg_loss"])) < 1e-5
+    for name, p in P.items():
+        gh = d["grad_head/" + name] if ("grad_head/" + name) in d.files else np.zeros(8)
+        atol = np.where(np.abs(gh[: p.numel()]) < 1e-6, 2 * 2.1 * 5e-4, 2e-5)
+        ok, e = _close(p.reshape(-1)[:8].numpy(), d["param_head/" + name], 1e-5, atol)
+        assert ok, (name, e)
