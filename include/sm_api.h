@@ -1,0 +1,138 @@
+/* C ABI of libsslmae.so — the MI355X (gfx950) kernels of the video-MAE
+ * pretraining step of lzc452/SSL-VIT-VIDEO-ANALYTICS.
+ *
+ * The reference has no FFI: its path is the Python module API used by
+ * src/train_ssl_mae.py:13-16 (tiny_vit_21m_variant, TinyVideoMAE, get_tube_mask,
+ * patchify) on stock aten ops.  Each entry point below replaces one aten op (or
+ * a fused group of them) on that path; the citation is the reference line whose
+ * computation it performs.  The host mirror of the reference API
+ * (ssl-vit-video-analytics_amd/ssl_mae_amd) binds these with ctypes.
+ *
+ * Conventions: raw device pointers, element counts, row strides in ELEMENTS,
+ * dtype enum (0 = f32, 1 = bf16), the caller's hipStream_t; kernels never
+ * allocate — scratch comes from the caller (`*_workspace_bytes`).  Every
+ * function returns 0 on success, a hipError_t (>0) on launch failure, or a
+ * negative code: -2 unsupported shape/alignment, -3 unsupported dtype combo,
+ * -4 workspace too small.  No exceptions cross the ABI; no host syncs.
+ */
+#ifndef SM_API_H
+#define SM_API_H
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- GEMM: every nn.Linear / 1x1 Conv2d and their dX/dW products.
+ * Replaces aten::addmm/mm of tiny_vit.py:79,81,93,94 (Mlp, Attention qkv/proj),
+ * tiny_vit.py:43,49 (MBConv 1x1 convs), mae_vit_adapter.py:24,53 (enc_to_dec,
+ * decoder_pred) and torch TransformerEncoderLayer in_proj/out_proj/linear1/2.
+ * C = alpha*op(A)op(B) + bias (+ beta*R, R = C when null); epi bit0 = exact GELU
+ * (aux <- pre-activation), bit1 = round the branch to bf16 before adding R (autocast).
+ * a_layout 0: A[M][K], 1: A[K][M];  b_layout 0: B[N][K], 1: B[K][N]. */
+int64_t sm_gemm_workspace_bytes(int ab_dtype, int M, int N, int K);
+int sm_gemm(int ab_dtype, int c_dtype, int a_layout, int b_layout, int M, int N, int K,
+            const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc,
+            const float* bias, float alpha, float beta, int epi, void* aux, const void* R,
+            void* workspace, int64_t ws_bytes, hipStream_t stream);
+
+/* ---- fused attention (tiny_vit.py:103 F.scaled_dot_product_attention;
+ * torch MultiheadAttention core of the decoder, mae_vit_adapter.py:40-48).
+ * qkv packed [N][L][3][H][D] bf16|f32, out O [N][L][H][D], lse [N][H][L]. */
+int sm_attn_fwd(int dtype, int N, int L, int H, int D, const void* qkv, void* out, float* lse,
+                float scale, float drop_p, uint64_t seed, hipStream_t st);
+int sm_attn_bwd(int dtype, int N, int L, int H, int D, const void* qkv, const void* o,
+                const void* dout, const float* lse, float* delta_ws /*[N][H][L]*/, void* dqkv,
+                float scale, float drop_p, uint64_t seed, hipStream_t st);
+
+/* ---- LayerNorm (tiny_vit.py:112,115; decoder norm1/norm2; mae_vit_adapter.py:50) */
+int sm_layernorm_fwd(int x_dtype, int y_dtype, int64_t M, int C, const void* x, const float* gamma,
+                     const float* beta, void* y, float* mean, float* rstd, float eps, hipStream_t st);
+int64_t sm_layernorm_bwd_workspace_bytes(int64_t M, int C);
+int sm_layernorm_bwd(int x_dtype, int dy_dtype, int dx_dtype, int64_t M, int C, const void* dy,
+                     const void* x, const float* mean, const float* rstd, const float* gamma,
+                     void* dx, const void* dres, float* dgamma, float* dbeta, void* ws,
+                     int64_t ws_bytes, hipStream_t st);
+
+/* ---- BatchNorm2d, train mode (tiny_vit.py:16 Conv2d_BN), channels-last [M][C] */
+int64_t sm_bn_workspace_bytes(int64_t M, int C);
+int sm_bn_stats(int x_dtype, int64_t M, int C, const void* x, float* mean, float* rstd,
+                float* run_mean, float* run_var, float momentum, float eps, int updates, void* ws,
+                int64_t ws_bytes, hipStream_t st);
+int sm_bn_apply(int x_dtype, int y_dtype, int64_t M, int C, const void* x, const float* mean,
+                const float* rstd, const float* w, const float* b, void* y, int gelu, const void* R,
+                hipStream_t st);
+int sm_bn_bwd(int x_dtype, int g_dtype, int64_t M, int C, const void* dy, const void* x,
+              const float* mean, const float* rstd, const float* w, const float* b, int gelu,
+              void* dx, float* dw, float* db, void* ws, int64_t ws_bytes, hipStream_t st);
+
+/* ---- elementwise (GELU tiny_vit.py:44,47,68,80; residual adds; casts) */
+int sm_gelu_bwd(int pre_dtype, int g_dtype, int64_t n, const void* pre, const void* dy, void* dx,
+                hipStream_t st);
+int sm_add(int a_dtype, int o_dtype, int64_t n, const void* a, const void* b, void* o, hipStream_t st);
+int sm_cast(int a_dtype, int o_dtype, int64_t n, const void* a, void* o, hipStream_t st);
+int sm_fill(float* p, int64_t n, float v, hipStream_t st);
+int sm_gelu_fwd(int dtype, int64_t n, const void* x, void* y, hipStream_t st);
+/* column sums (Linear bias gradients): out[c] (+)= sum_m x[m][c] */
+int64_t sm_colsum_workspace_bytes(int64_t M, int C);
+int sm_colsum(int dtype, int64_t M, int C, const void* x, float* out, int accumulate, void* ws,
+              int64_t ws_bytes, hipStream_t st);
+
+/* ---- convolutions (PatchEmbed tiny_vit.py:62-72; depthwise 3x3 tiny_vit.py:46)
+ * stem im2col folds the frame permute of mae_vit_adapter.py:84 into its loads. */
+int sm_stem_im2col(int out_dtype, const float* clip, int B, int T, int H, int W, int64_t sB,
+                   int64_t sC, int64_t sT, int64_t sH, int64_t sW, int stride, void* col, hipStream_t st);
+int sm_im2col3(int dtype, const void* x, int F, int H, int W, int C, int stride, void* col, hipStream_t st);
+int sm_col2im3(int dtype, const void* dcol, int F, int H, int W, int C, int stride, void* dx, hipStream_t st);
+int sm_conv_wpack(int out_dtype, const float* src, void* dst, int Cout, int Cin, int Kpad, int order,
+                  hipStream_t st);
+int sm_conv_wunpack_add(const float* packed, float* grad, int Cout, int Cin, int Kpad, int order,
+                        hipStream_t st);
+int sm_dwconv_fwd(int dtype, const void* x, const float* w, void* y, int F, int H, int W, int C,
+                  int stride, hipStream_t st);
+int64_t sm_dwconv_wgrad_workspace_bytes(int F, int H, int W, int C, int stride);
+int sm_dwconv_bwd(int dtype, const void* dy, const void* x, const float* w, void* dx, float* dw, int F,
+                  int H, int W, int C, int stride, void* ws, int64_t ws_bytes, hipStream_t st);
+
+/* ---- SELayer (tiny_vit.py:20-34) */
+int sm_se_fwd(int dtype, const void* x, int F, int HW, int C, int R, const float* w1, const float* w2,
+              float* pooled, float* z1, float* s, void* y, hipStream_t st);
+int sm_se_bwd(int dtype, const void* dy, const void* x, int F, int HW, int C, int R, const float* w1,
+              const float* w2, const float* s, const float* z1, float* ds_ws, float* dz2, float* dz1,
+              float* dpool_ws, void* dx, hipStream_t st);
+int sm_se_scale(int dtype, const void* x, const float* s, void* y, int F, int HW, int C, hipStream_t st);
+
+/* ---- MAE glue: tube mask (mae_loader.py:80-90) + masked-token compaction
+ * (train_ssl_mae.py:105), pos-embed/mask-token blend (mae_vit_adapter.py:97-104),
+ * fused patchify + norm_pix + masked MSE (train_ssl_mae.py:26-31,74-84). */
+int sm_tube_mask(const float* noise, int B, int T, int L, int n_mask, uint8_t* mask, int32_t* idx,
+                 hipStream_t st);
+int sm_pos_blend_fwd(int y_dtype, int x_dtype, const void* y, const float* tpos, const float* spos,
+                     const float* tok, const uint8_t* mask, void* x, int B, int T, int L, int D,
+                     hipStream_t st);
+int sm_pos_blend_bwd(int g_dtype, int y_dtype, const void* dx, const uint8_t* mask, void* dy,
+                     float* dtpos, float* dspos, float* dtok, float* ws, int B, int T, int L, int D,
+                     hipStream_t st);
+int64_t sm_loss_workspace_bytes(int B, int T, int L);
+int sm_mae_loss_fwd(int pred_dtype, const void* pred, const float* clip, int64_t sB, int64_t sC,
+                    int64_t sT, int64_t sH, int64_t sW, const uint8_t* mask, int B, int T, int H, int W,
+                    int norm_pix, float* loss, float* denom, void* ws, int64_t ws_bytes, hipStream_t st);
+int sm_mae_loss_bwd(int pred_dtype, const void* pred, const float* clip, int64_t sB, int64_t sC,
+                    int64_t sT, int64_t sH, int64_t sW, const uint8_t* mask, int B, int T, int H, int W,
+                    int norm_pix, const float* grad_out, const float* denom, void* dpred, hipStream_t st);
+int sm_gather_rows(int dtype, const void* src, const int32_t* idx, int64_t nrows, int C, void* dst,
+                   hipStream_t st);
+int64_t sm_std_workspace_bytes(void);
+int sm_std(int dtype, const void* x, int64_t n, float* out, void* ws, int64_t ws_bytes, hipStream_t st);
+
+/* ---- optimizer (train_ssl_mae.py:163 AdamW, :87-89 GradScaler inf-skip) */
+int sm_nonfinite(const float* g, int64_t n, int* flag, hipStream_t st);
+int sm_adamw(float* p, const float* g, float* m, float* v, void* bf16_shadow, int64_t n, float lr,
+             float b1, float b2, float eps, float wd, const int* found_inf, int64_t* step,
+             hipStream_t st);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SM_API_H */

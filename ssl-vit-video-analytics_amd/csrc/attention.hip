@@ -1,0 +1,606 @@
+// Fused multi-head attention (flash-style, no score matrix in HBM), forward and
+// backward, for the TinyViT encoder (head_dim 32, L = 3136 / 784, reference
+// tiny_vit.py:86-106 -> F.scaled_dot_product_attention) and the MAE decoder
+// (head_dim 64, L = T*784, torch MultiheadAttention inside
+// nn.TransformerEncoderLayer, mae_vit_adapter.py:40-48).
+//
+// Operands are read straight out of the packed projection output
+//   qkv[n][l][3][h][d]      (row stride 3*H*D)        — Linear(C, 3C) output
+// and the output is written as O[n][l][h][d] (= [N*L, C]), i.e. exactly the
+// `transpose(1,2).reshape(B,L,C)` layout the following projection consumes, so
+// no permute copies exist anywhere.  LSE[n][h][l] (natural log, fp32) is kept
+// for the backward.  Backward writes dqkv in the same packed layout.
+//
+// bf16 kernels: 4 waves x 32 query rows, 64-key tiles in LDS.  The score tile is
+// computed transposed (S^T = K Q^T on v_mfma_f32_32x32x16_bf16) so each lane owns
+// one query column: the online-softmax max/sum are in-register plus one
+// cross-half exchange, the per-row rescale is a per-lane multiply, and P^T feeds
+// the P.V MFMA directly from the accumulator registers.  V (and in the backward
+// Q / dO / K) are read transposed from LDS with ds_read_b64_tr_b16.
+//
+// f32 kernels (parity mode): one thread per query (fwd, dQ) or key (dK/dV) with
+// LDS-staged tiles; exact fp32.
+#include "common.h"
+#include "sm_api.h"
+
+namespace {
+
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+constexpr float NEG_BIG = -1e30f;
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+
+struct AttnArgs {
+  const void* qkv;   // [N][L][3][H][D]
+  void* out;         // fwd: O [N][L][H][D]; bwd: dqkv [N][L][3][H][D]
+  const void* o;     // bwd: O
+  const void* dout;  // bwd: dO [N][L][H][D]
+  float* lse;        // [N][H][L]
+  float* delta;      // [N][H][L]  rowsum(dO * O)
+  int N, L, H;
+  float scale;
+  float drop_p;      // dropout on attention probabilities (0 = off)
+  uint64_t seed;
+};
+
+// ---------- LDS images for a [rows][D] bf16 tile (row = key or query) -------------
+// Row reads (ds_read_b128 of 8 consecutive d) and transposed reads
+// (ds_read_b64_tr_b16 of 4 consecutive rows) both address through tile_off.
+template <int D>
+SM_DEV int tile_off(int row, int d) {
+  constexpr int CPR = D / 8;              // 16-B chunks per row
+  int chunk = d >> 3;
+  if (D == 64) chunk ^= (((row >> 1) & 1) << 2) ^ ((row >> 2) & 3);
+  else chunk ^= (row >> 2) & 3;
+  return row * (D * 2) + (chunk << 4) + ((d & 7) << 1);
+  (void)CPR;
+}
+
+template <int D>
+SM_DEV bf16x8 row_frag(const char* lds, int row, int s) {
+  const int h = (threadIdx.x & 63) >> 5;
+  return *(const bf16x8*)(lds + tile_off<D>(row, 16 * s + 8 * h));
+}
+
+// A-operand fragment of X^T where X is the [rows][D] tile: lane (r = column d of
+// X, h) element j = X[rb + 16 s + 8 (j>>2) + 4 h + (j&3)][db + r].
+template <int D>
+SM_DEV bf16x8 tr_frag(const char* lds, int rb, int db, int s) {
+  const int l = threadIdx.x & 63;
+  const int h = l >> 5, g1 = (l >> 4) & 1, i = l & 15, q = i >> 2, p = i & 3;
+  const int col = db + 16 * g1 + 4 * p;
+  const int r0 = rb + 16 * s + 4 * h + q;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + tile_off<D>(r0, col)));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + tile_off<D>(r0 + 8, col)));
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// Stage rows [r0, r0+ROWS) of a [L][ld] bf16 matrix (column offset folded into base)
+// into the LDS image; rows >= L are zero.
+template <int D, int ROWS>
+SM_DEV void stage_rows(char* lds, const __bf16* base, int64_t ld, int r0, int L) {
+  constexpr int CHUNKS = ROWS * D / 8;
+  for (int c = threadIdx.x; c < CHUNKS; c += 256) {
+    const int row = c / (D / 8), d = (c % (D / 8)) * 8;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r0 + row < L) v = *(const uint4*)(base + (int64_t)(r0 + row) * ld + d);
+    *(uint4*)(lds + tile_off<D>(row, d)) = v;
+  }
+}
+
+// accumulator (32x32) -> bf16 B-operand fragment for k-step s
+SM_DEV bf16x8 acc_to_frag(const f32x16& a, int s) {
+  bf16x8 f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = (__bf16)a[8 * s + j];
+  return f;
+}
+SM_DEV int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+SM_DEV float drop_keep_scale(const AttnArgs& a, int n, int hd, int q, int k) {
+  // dropout mask on the attention probability P[n,hd,q,k]
+  const uint64_t idx = (((uint64_t)(n * a.H + hd) * a.L + q) * (uint64_t)a.L) + k;
+  return uniform01(a.seed, idx) >= a.drop_p ? 1.0f / (1.0f - a.drop_p) : 0.0f;
+}
+
+// =============================================================== bf16 forward
+template <int D, bool DROP>
+__global__ __launch_bounds__(256) void attn_fwd_bf16(AttnArgs a) {
+  constexpr int KT = 64;
+  __shared__ __attribute__((aligned(16))) char lk[KT * D * 2];
+  __shared__ __attribute__((aligned(16))) char lv[KT * D * 2];
+  const int n = blockIdx.z, hd = blockIdx.y;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5;
+  const int C = a.H * D;
+  const int64_t ldq = 3 * (int64_t)C;
+  const __bf16* qkv = (const __bf16*)a.qkv + (int64_t)n * a.L * ldq;
+  const __bf16* qb = qkv + hd * D;
+  const __bf16* kb = qkv + C + hd * D;
+  const __bf16* vb = qkv + 2 * C + hd * D;
+  const int q = blockIdx.x * 128 + w * 32 + (l & 31);
+
+  bf16x8 qf[D / 16];
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    if (q < a.L) qf[s] = *(const bf16x8*)(qb + (int64_t)q * ldq + 16 * s + 8 * h);
+    else for (int j = 0; j < 8; ++j) qf[s][j] = (__bf16)0.f;
+  }
+  f32x16 o[D / 32];
+#pragma unroll
+  for (int t = 0; t < D / 32; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[t][r] = 0.f;
+  float m = NEG_BIG, lsum = 0.f;
+  const float c = a.scale * LOG2E;
+
+  for (int k0 = 0; k0 < a.L; k0 += KT) {
+    __syncthreads();
+    stage_rows<D, KT>(lk, kb, ldq, k0, a.L);
+    stage_rows<D, KT>(lv, vb, ldq, k0, a.L);
+    __syncthreads();
+    f32x16 st[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) st[u][r] = 0.f;
+#pragma unroll
+      for (int s = 0; s < D / 16; ++s)
+        st[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(lk, 32 * u + (l & 31), s), qf[s],
+                                                         st[u], 0, 0, 0);
+    }
+    float mt = NEG_BIG;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = k0 + 32 * u + acc_row(r, h);
+        float x = st[u][r] * c;
+        if (key >= a.L) x = NEG_BIG;
+        st[u][r] = x;
+        mt = fmaxf(mt, x);
+      }
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float mn = fmaxf(m, mt);
+    const float alpha = exp2f(m - mn);
+    m = mn;
+    float ps = 0.f;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float p = exp2f(st[u][r] - mn);
+        ps += p;
+        if (DROP) p *= drop_keep_scale(a, n, hd, q, k0 + 32 * u + acc_row(r, h));
+        st[u][r] = p;
+      }
+    lsum = lsum * alpha + ps;
+#pragma unroll
+    for (int t = 0; t < D / 32; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pf = acc_to_frag(st[u], s);
+#pragma unroll
+        for (int t = 0; t < D / 32; ++t)
+          o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(lv, 32 * u, 32 * t, s), pf, o[t], 0, 0, 0);
+      }
+  }
+  lsum += __shfl_xor(lsum, 32, 64);
+  if (q < a.L) {
+    const float inv = 1.f / lsum;
+    __bf16* ob = (__bf16*)a.out + ((int64_t)n * a.L + q) * C + hd * D;
+#pragma unroll
+    for (int t = 0; t < D / 32; ++t)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = o[t][4 * g + i] * inv;
+        store4(ob + 32 * t + 8 * g + 4 * h, v);
+      }
+    if (h == 0) a.lse[((int64_t)n * a.H + hd) * a.L + q] = (m + log2f(lsum)) * LN2;
+  }
+}
+
+// =============================================================== delta = rowsum(dO*O)
+template <typename T>
+__global__ void attn_delta_kernel(AttnArgs a, int D) {
+  // one wave per (n, l) row: H*D values; lanes split over heads
+  const int64_t row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int l = threadIdx.x & 63;
+  if (row >= (int64_t)a.N * a.L) return;
+  const int C = a.H * D;
+  const T* o = (const T*)a.o + row * C;
+  const T* dout = (const T*)a.dout + row * C;
+  const int n = (int)(row / a.L), q = (int)(row % a.L);
+  for (int hd = 0; hd < a.H; ++hd) {
+    float s = 0.f;
+    for (int d = l; d < D; d += 64) s += to_f<T>(o[hd * D + d]) * to_f<T>(dout[hd * D + d]);
+    s = wave_sum(s);
+    if (l == 0) a.delta[((int64_t)n * a.H + hd) * a.L + q] = s;
+  }
+}
+
+// =============================================================== bf16 backward dK, dV
+template <int D, bool DROP>
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(AttnArgs a) {
+  constexpr int QT = 64;
+  __shared__ __attribute__((aligned(16))) char lq[QT * D * 2];
+  __shared__ __attribute__((aligned(16))) char ldo[QT * D * 2];
+  __shared__ float llse[QT], ldel[QT];
+  const int n = blockIdx.z, hd = blockIdx.y;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5;
+  const int C = a.H * D;
+  const int64_t ldq = 3 * (int64_t)C;
+  const __bf16* qkv = (const __bf16*)a.qkv + (int64_t)n * a.L * ldq;
+  const __bf16* qb = qkv + hd * D;
+  const __bf16* kb = qkv + C + hd * D;
+  const __bf16* vb = qkv + 2 * C + hd * D;
+  const __bf16* dob = (const __bf16*)a.dout + (int64_t)n * a.L * C + hd * D;
+  const float* lse = a.lse + ((int64_t)n * a.H + hd) * a.L;
+  const float* del = a.delta + ((int64_t)n * a.H + hd) * a.L;
+  const int key = blockIdx.x * 128 + w * 32 + (l & 31);
+
+  bf16x8 kf[D / 16], vf[D / 16];
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    if (key < a.L) {
+      kf[s] = *(const bf16x8*)(kb + (int64_t)key * ldq + 16 * s + 8 * h);
+      vf[s] = *(const bf16x8*)(vb + (int64_t)key * ldq + 16 * s + 8 * h);
+    } else {
+      for (int j = 0; j < 8; ++j) { kf[s][j] = (__bf16)0.f; vf[s][j] = (__bf16)0.f; }
+    }
+  }
+  f32x16 dk[D / 32], dv[D / 32];
+#pragma unroll
+  for (int t = 0; t < D / 32; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { dk[t][r] = 0.f; dv[t][r] = 0.f; }
+  const float c = a.scale * LOG2E;
+
+  for (int q0 = 0; q0 < a.L; q0 += QT) {
+    __syncthreads();
+    stage_rows<D, QT>(lq, qb, ldq, q0, a.L);
+    stage_rows<D, QT>(ldo, dob, C, q0, a.L);
+    if (threadIdx.x < QT) {
+      const int qq = q0 + threadIdx.x;
+      llse[threadIdx.x] = qq < a.L ? lse[qq] * LOG2E : 1e30f;   // invalid rows -> P = 0
+      ldel[threadIdx.x] = qq < a.L ? del[qq] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      f32x16 sacc, dpacc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { sacc[r] = 0.f; dpacc[r] = 0.f; }
+#pragma unroll
+      for (int s = 0; s < D / 16; ++s) {
+        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(lq, 32 * u + (l & 31), s), kf[s], sacc, 0, 0, 0);
+        dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(ldo, 32 * u + (l & 31), s), vf[s], dpacc, 0, 0, 0);
+      }
+      // rows = queries (regs), column = this lane's key
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qi = 32 * u + acc_row(r, h);
+        float p = exp2f(sacc[r] * c - llse[qi]);
+        float dp = dpacc[r];
+        if (DROP) {
+          const float ks = (q0 + qi < a.L) ? drop_keep_scale(a, n, hd, q0 + qi, key) : 0.f;
+          dp *= ks;
+          sacc[r] = p * ks;              // dropped P feeds dV
+        } else {
+          sacc[r] = p;
+        }
+        dpacc[r] = p * (dp - ldel[qi]);  // dS
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pf = acc_to_frag(sacc, s);
+        const bf16x8 sf = acc_to_frag(dpacc, s);
+#pragma unroll
+        for (int t = 0; t < D / 32; ++t) {
+          dv[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(ldo, 32 * u, 32 * t, s), pf, dv[t], 0, 0, 0);
+          dk[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(lq, 32 * u, 32 * t, s), sf, dk[t], 0, 0, 0);
+        }
+      }
+    }
+  }
+  if (key < a.L) {
+    __bf16* out = (__bf16*)a.out + ((int64_t)n * a.L + key) * ldq + hd * D;
+#pragma unroll
+    for (int t = 0; t < D / 32; ++t)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float vk[4], vv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { vk[i] = dk[t][4 * g + i] * a.scale; vv[i] = dv[t][4 * g + i]; }
+        store4(out + C + 32 * t + 8 * g + 4 * h, vk);
+        store4(out + 2 * C + 32 * t + 8 * g + 4 * h, vv);
+      }
+  }
+}
+
+// =============================================================== bf16 backward dQ
+template <int D, bool DROP>
+__global__ __launch_bounds__(256) void attn_bwd_dq_bf16(AttnArgs a) {
+  constexpr int KT = 64;
+  __shared__ __attribute__((aligned(16))) char lk[KT * D * 2];
+  __shared__ __attribute__((aligned(16))) char lv[KT * D * 2];
+  const int n = blockIdx.z, hd = blockIdx.y;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5;
+  const int C = a.H * D;
+  const int64_t ldq = 3 * (int64_t)C;
+  const __bf16* qkv = (const __bf16*)a.qkv + (int64_t)n * a.L * ldq;
+  const __bf16* qb = qkv + hd * D;
+  const __bf16* kb = qkv + C + hd * D;
+  const __bf16* vb = qkv + 2 * C + hd * D;
+  const __bf16* dob = (const __bf16*)a.dout + (int64_t)n * a.L * C + hd * D;
+  const int q = blockIdx.x * 128 + w * 32 + (l & 31);
+  const bool qok = q < a.L;
+  const float lse2 = qok ? a.lse[((int64_t)n * a.H + hd) * a.L + q] * LOG2E : 1e30f;
+  const float dl = qok ? a.delta[((int64_t)n * a.H + hd) * a.L + q] : 0.f;
+
+  bf16x8 qf[D / 16], df[D / 16];
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    if (qok) {
+      qf[s] = *(const bf16x8*)(qb + (int64_t)q * ldq + 16 * s + 8 * h);
+      df[s] = *(const bf16x8*)(dob + (int64_t)q * C + 16 * s + 8 * h);
+    } else {
+      for (int j = 0; j < 8; ++j) { qf[s][j] = (__bf16)0.f; df[s][j] = (__bf16)0.f; }
+    }
+  }
+  f32x16 dq[D / 32];
+#pragma unroll
+  for (int t = 0; t < D / 32; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dq[t][r] = 0.f;
+  const float c = a.scale * LOG2E;
+
+  for (int k0 = 0; k0 < a.L; k0 += KT) {
+    __syncthreads();
+    stage_rows<D, KT>(lk, kb, ldq, k0, a.L);
+    stage_rows<D, KT>(lv, vb, ldq, k0, a.L);
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      f32x16 sacc, dpacc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { sacc[r] = 0.f; dpacc[r] = 0.f; }
+#pragma unroll
+      for (int s = 0; s < D / 16; ++s) {
+        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(lk, 32 * u + (l & 31), s), qf[s], sacc, 0, 0, 0);
+        dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(lv, 32 * u + (l & 31), s), df[s], dpacc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = k0 + 32 * u + acc_row(r, h);
+        float p = key < a.L ? exp2f(sacc[r] * c - lse2) : 0.f;
+        float dp = dpacc[r];
+        if (DROP) dp *= (key < a.L && qok) ? drop_keep_scale(a, n, hd, q, key) : 0.f;
+        dpacc[r] = p * (dp - dl);
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 sf = acc_to_frag(dpacc, s);
+#pragma unroll
+        for (int t = 0; t < D / 32; ++t)
+          dq[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(lk, 32 * u, 32 * t, s), sf, dq[t], 0, 0, 0);
+      }
+    }
+  }
+  if (qok) {
+    __bf16* out = (__bf16*)a.out + ((int64_t)n * a.L + q) * ldq + hd * D;
+#pragma unroll
+    for (int t = 0; t < D / 32; ++t)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = dq[t][4 * g + i] * a.scale;
+        store4(out + 32 * t + 8 * g + 4 * h, v);
+      }
+  }
+}
+
+// =============================================================== f32 kernels
+template <int D>
+__global__ __launch_bounds__(128) void attn_fwd_f32(AttnArgs a) {
+  constexpr int KT = 32;
+  __shared__ float lk[KT][D], lv[KT][D];
+  const int n = blockIdx.z, hd = blockIdx.y;
+  const int C = a.H * D;
+  const int64_t ldq = 3 * (int64_t)C;
+  const float* qkv = (const float*)a.qkv + (int64_t)n * a.L * ldq;
+  const int q = blockIdx.x * 128 + threadIdx.x;
+  const bool qok = q < a.L;
+  float qv[D], o[D];
+  for (int d = 0; d < D; ++d) { qv[d] = qok ? qkv[(int64_t)q * ldq + hd * D + d] : 0.f; o[d] = 0.f; }
+  float m = NEG_BIG, lsum = 0.f;
+  for (int k0 = 0; k0 < a.L; k0 += KT) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < KT * D; i += 128) {
+      const int r = i / D, d = i % D, key = k0 + r;
+      lk[r][d] = key < a.L ? qkv[(int64_t)key * ldq + C + hd * D + d] : 0.f;
+      lv[r][d] = key < a.L ? qkv[(int64_t)key * ldq + 2 * C + hd * D + d] : 0.f;
+    }
+    __syncthreads();
+    for (int r = 0; r < KT && k0 + r < a.L; ++r) {
+      float s = 0.f;
+      for (int d = 0; d < D; ++d) s += qv[d] * lk[r][d];
+      s *= a.scale;
+      const float mn = fmaxf(m, s);
+      const float al = __expf(m - mn);
+      float p = __expf(s - mn);
+      lsum = lsum * al + p;
+      if (a.drop_p > 0.f) p *= drop_keep_scale(a, n, hd, q, k0 + r);
+      for (int d = 0; d < D; ++d) o[d] = o[d] * al + p * lv[r][d];
+      m = mn;
+    }
+  }
+  if (qok) {
+    float* ob = (float*)a.out + ((int64_t)n * a.L + q) * C + hd * D;
+    for (int d = 0; d < D; ++d) ob[d] = o[d] / lsum;
+    a.lse[((int64_t)n * a.H + hd) * a.L + q] = m + logf(lsum);
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(128) void attn_bwd_dq_f32(AttnArgs a) {
+  constexpr int KT = 32;
+  __shared__ float lk[KT][D], lv[KT][D];
+  const int n = blockIdx.z, hd = blockIdx.y;
+  const int C = a.H * D;
+  const int64_t ldq = 3 * (int64_t)C;
+  const float* qkv = (const float*)a.qkv + (int64_t)n * a.L * ldq;
+  const float* dob = (const float*)a.dout + (int64_t)n * a.L * C;
+  const int q = blockIdx.x * 128 + threadIdx.x;
+  const bool qok = q < a.L;
+  float qv[D], dov[D], dq[D];
+  for (int d = 0; d < D; ++d) {
+    qv[d] = qok ? qkv[(int64_t)q * ldq + hd * D + d] : 0.f;
+    dov[d] = qok ? dob[(int64_t)q * C + hd * D + d] : 0.f;
+    dq[d] = 0.f;
+  }
+  const float lse = qok ? a.lse[((int64_t)n * a.H + hd) * a.L + q] : 0.f;
+  const float dl = qok ? a.delta[((int64_t)n * a.H + hd) * a.L + q] : 0.f;
+  for (int k0 = 0; k0 < a.L; k0 += KT) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < KT * D; i += 128) {
+      const int r = i / D, d = i % D, key = k0 + r;
+      lk[r][d] = key < a.L ? qkv[(int64_t)key * ldq + C + hd * D + d] : 0.f;
+      lv[r][d] = key < a.L ? qkv[(int64_t)key * ldq + 2 * C + hd * D + d] : 0.f;
+    }
+    __syncthreads();
+    for (int r = 0; r < KT && k0 + r < a.L; ++r) {
+      float s = 0.f, dp = 0.f;
+      for (int d = 0; d < D; ++d) { s += qv[d] * lk[r][d]; dp += dov[d] * lv[r][d]; }
+      const float p = __expf(s * a.scale - lse);
+      if (a.drop_p > 0.f) dp *= drop_keep_scale(a, n, hd, q, k0 + r);
+      const float ds = p * (dp - dl);
+      for (int d = 0; d < D; ++d) dq[d] += ds * lk[r][d];
+    }
+  }
+  if (qok) {
+    float* out = (float*)a.out + ((int64_t)n * a.L + q) * ldq + hd * D;
+    for (int d = 0; d < D; ++d) out[d] = dq[d] * a.scale;
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(128) void attn_bwd_dkdv_f32(AttnArgs a) {
+  constexpr int QT = 32;
+  __shared__ float lq[QT][D], ldo[QT][D], llse[QT], ldel[QT];
+  const int n = blockIdx.z, hd = blockIdx.y;
+  const int C = a.H * D;
+  const int64_t ldq = 3 * (int64_t)C;
+  const float* qkv = (const float*)a.qkv + (int64_t)n * a.L * ldq;
+  const float* dob = (const float*)a.dout + (int64_t)n * a.L * C;
+  const int key = blockIdx.x * 128 + threadIdx.x;
+  const bool kok = key < a.L;
+  float kv[D], vv[D], dk[D], dv[D];
+  for (int d = 0; d < D; ++d) {
+    kv[d] = kok ? qkv[(int64_t)key * ldq + C + hd * D + d] : 0.f;
+    vv[d] = kok ? qkv[(int64_t)key * ldq + 2 * C + hd * D + d] : 0.f;
+    dk[d] = 0.f; dv[d] = 0.f;
+  }
+  for (int q0 = 0; q0 < a.L; q0 += QT) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < QT * D; i += 128) {
+      const int r = i / D, d = i % D, qq = q0 + r;
+      lq[r][d] = qq < a.L ? qkv[(int64_t)qq * ldq + hd * D + d] : 0.f;
+      ldo[r][d] = qq < a.L ? dob[(int64_t)qq * C + hd * D + d] : 0.f;
+    }
+    if (threadIdx.x < QT) {
+      const int qq = q0 + threadIdx.x;
+      llse[threadIdx.x] = qq < a.L ? a.lse[((int64_t)n * a.H + hd) * a.L + qq] : 0.f;
+      ldel[threadIdx.x] = qq < a.L ? a.delta[((int64_t)n * a.H + hd) * a.L + qq] : 0.f;
+    }
+    __syncthreads();
+    for (int r = 0; r < QT && q0 + r < a.L; ++r) {
+      float s = 0.f, dp = 0.f;
+      for (int d = 0; d < D; ++d) { s += lq[r][d] * kv[d]; dp += ldo[r][d] * vv[d]; }
+      const float p = __expf(s * a.scale - llse[r]);
+      float pd = p;
+      if (a.drop_p > 0.f) {
+        const float ks = drop_keep_scale(a, n, hd, q0 + r, key);
+        pd = p * ks;
+        dp *= ks;
+      }
+      const float ds = p * (dp - ldel[r]);
+      for (int d = 0; d < D; ++d) { dv[d] += pd * ldo[r][d]; dk[d] += ds * lq[r][d]; }
+    }
+  }
+  if (kok) {
+    float* out = (float*)a.out + ((int64_t)n * a.L + key) * ldq + hd * D;
+    for (int d = 0; d < D; ++d) { out[C + d] = dk[d] * a.scale; out[2 * C + d] = dv[d]; }
+  }
+}
+
+}  // namespace
+
+extern "C" int sm_attn_fwd(int dtype, int N, int L, int H, int D, const void* qkv, void* out,
+                           float* lse, float scale, float drop_p, uint64_t seed, hipStream_t st) {
+  if (N <= 0 || L <= 0) return 0;
+  if (D != 32 && D != 64) return -2;
+  AttnArgs a{};
+  a.qkv = qkv; a.out = out; a.lse = lse; a.N = N; a.L = L; a.H = H; a.scale = scale;
+  a.drop_p = drop_p; a.seed = seed;
+  dim3 grid((L + 127) / 128, H, N);
+  const bool drop = drop_p > 0.f;
+  if (dtype == SM_BF16) {
+    if (D == 32) {
+      if (drop) hipLaunchKernelGGL((attn_fwd_bf16<32, true>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((attn_fwd_bf16<32, false>), grid, dim3(256), 0, st, a);
+    } else {
+      if (drop) hipLaunchKernelGGL((attn_fwd_bf16<64, true>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((attn_fwd_bf16<64, false>), grid, dim3(256), 0, st, a);
+    }
+  } else {
+    if (D == 32) hipLaunchKernelGGL(attn_fwd_f32<32>, grid, dim3(128), 0, st, a);
+    else hipLaunchKernelGGL(attn_fwd_f32<64>, grid, dim3(128), 0, st, a);
+  }
+  SM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int sm_attn_bwd(int dtype, int N, int L, int H, int D, const void* qkv, const void* o,
+                           const void* dout, const float* lse, float* delta_ws, void* dqkv,
+                           float scale, float drop_p, uint64_t seed, hipStream_t st) {
+  if (N <= 0 || L <= 0) return 0;
+  if (D != 32 && D != 64) return -2;
+  AttnArgs a{};
+  a.qkv = qkv; a.o = o; a.dout = dout; a.lse = (float*)lse; a.delta = delta_ws; a.out = dqkv;
+  a.N = N; a.L = L; a.H = H; a.scale = scale; a.drop_p = drop_p; a.seed = seed;
+  const int64_t rows = (int64_t)N * L;
+  const int dblocks = (int)((rows + 3) / 4);
+  if (dtype == SM_BF16) hipLaunchKernelGGL(attn_delta_kernel<__bf16>, dim3(dblocks), dim3(256), 0, st, a, D);
+  else hipLaunchKernelGGL(attn_delta_kernel<float>, dim3(dblocks), dim3(256), 0, st, a, D);
+  SM_CHECK_LAUNCH();
+  dim3 grid((L + 127) / 128, H, N);
+  const bool drop = drop_p > 0.f;
+  if (dtype == SM_BF16) {
+#define SM_ATTN_BWD(DD, DR)                                                        \
+  hipLaunchKernelGGL((attn_bwd_dkdv_bf16<DD, DR>), grid, dim3(256), 0, st, a);    \
+  hipLaunchKernelGGL((attn_bwd_dq_bf16<DD, DR>), grid, dim3(256), 0, st, a);
+    if (D == 32) { if (drop) { SM_ATTN_BWD(32, true) } else { SM_ATTN_BWD(32, false) } }
+    else { if (drop) { SM_ATTN_BWD(64, true) } else { SM_ATTN_BWD(64, false) } }
+#undef SM_ATTN_BWD
+  } else {
+    if (D == 32) {
+      hipLaunchKernelGGL(attn_bwd_dkdv_f32<32>, grid, dim3(128), 0, st, a);
+      hipLaunchKernelGGL(attn_bwd_dq_f32<32>, grid, dim3(128), 0, st, a);
+    } else {
+      hipLaunchKernelGGL(attn_bwd_dkdv_f32<64>, grid, dim3(128), 0, st, a);
+      hipLaunchKernelGGL(attn_bwd_dq_f32<64>, grid, dim3(128), 0, st, a);
+    }
+  }
+  SM_CHECK_LAUNCH();
+  return 0;
+}

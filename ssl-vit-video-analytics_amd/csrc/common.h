@@ -1,0 +1,115 @@
+// Shared device helpers for the MI355X (gfx950 / CDNA4) MAE kernels.
+// Storage types: float (parity mode) and __bf16 (training mode); every kernel
+// accumulates in fp32.  Wave = 64 lanes.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define SM_DEV __device__ __forceinline__
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+
+enum SmDtype { SM_F32 = 0, SM_BF16 = 1 };
+
+// ---------------------------------------------------------------- conversions
+template <typename T> SM_DEV float to_f(T x);
+template <> SM_DEV float to_f<float>(float x) { return x; }
+template <> SM_DEV float to_f<__bf16>(__bf16 x) { return (float)x; }
+template <typename T> SM_DEV T from_f(float x);
+template <> SM_DEV float from_f<float>(float x) { return x; }
+template <> SM_DEV __bf16 from_f<__bf16>(float x) { return (__bf16)x; }
+
+// 8-wide vector load/store of T as fp32 (16 B for bf16, 32 B for f32).
+SM_DEV void load8(const float* p, float* v) {
+  float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+SM_DEV void load8(const __bf16* p, float* v) {
+  bf16x8 a = *(const bf16x8*)p;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = (float)a[i];
+}
+SM_DEV void store8(float* p, const float* v) {
+  *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+  *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+SM_DEV void store8(__bf16* p, const float* v) {
+  bf16x8 a;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = (__bf16)v[i];
+  *(bf16x8*)p = a;
+}
+SM_DEV void load4(const float* p, float* v) {
+  float4 a = *(const float4*)p;
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+}
+SM_DEV void load4(const __bf16* p, float* v) {
+  bf16x4 a = *(const bf16x4*)p;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = (float)a[i];
+}
+SM_DEV void store4(float* p, const float* v) { *(float4*)p = make_float4(v[0], v[1], v[2], v[3]); }
+SM_DEV void store4(__bf16* p, const float* v) {
+  bf16x4 a;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) a[i] = (__bf16)v[i];
+  *(bf16x4*)p = a;
+}
+
+// ---------------------------------------------------------------- math
+SM_DEV float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+SM_DEV float gelu_grad(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+// ---------------------------------------------------------------- reductions
+SM_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+SM_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+SM_DEV double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Block-wide sum; `red` must hold blockDim.x/64 floats.  Result valid in all threads.
+SM_DEV float block_sum(float v, float* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += red[i];
+  return t;
+}
+
+// ---------------------------------------------------------------- counter RNG
+// Stateless 32-bit hash (used for dropout / drop-path masks): a keyed
+// splitmix-style mixer of (seed, offset).  Deterministic and replayable in bwd.
+SM_DEV uint32_t mix32(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed * 0x9E3779B97F4A7C15ull + idx + 0x632BE59BD9B4E019ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)(z >> 32);
+}
+SM_DEV float uniform01(uint64_t seed, uint64_t idx) {
+  return (mix32(seed, idx) >> 8) * (1.0f / 16777216.0f);
+}
+
+#define SM_CHECK_LAUNCH() \
+  do { hipError_t e__ = hipGetLastError(); if (e__ != hipSuccess) return (int)e__; } while (0)

@@ -1,0 +1,348 @@
+// General GEMM for the MAE step: every nn.Linear / 1x1-conv forward and both of
+// its backward products.
+//
+//   C[M,N] = beta*C + alpha * sum_k A(m,k) B(k,n) (+ bias[n]) (then optional GELU)
+//
+//   a_layout 0: A stored [M][K] (K contiguous)     1: A stored [K][M] (M contiguous)
+//   b_layout 0: B stored [N][K] (nn.Linear weight) 1: B stored [K][N] (N contiguous)
+//
+// Linear fwd  Y = X W^T      : (a 0, b 0)
+// Linear dX   dX = dY W      : (a 0, b 1)
+// Linear dW   dW = dY^T X    : (a 1, b 1)   -> split-K over the token axis
+//
+// bf16 path: 128x128x64 block tile, 4 waves (2x2), each wave 64x64 = 2x2
+// v_mfma_f32_32x32x16_bf16 tiles.  K-contiguous operands are staged to an
+// XOR-swizzled [row][64] LDS image read with ds_read_b128; M/N-contiguous operands
+// are staged as a [k][128] image and read with ds_read_b64_tr_b16 (hardware
+// transpose), so no operand ever needs a transposed copy in HBM.  Register-staged
+// prefetch of tile k+1 is issued before the MFMAs of tile k (async-STAGE split).
+// f32 path (parity mode): 64x64x16 tile on v_mfma_f32_32x32x2_f32 (exact fp32).
+#include "common.h"
+#include "sm_api.h"
+
+namespace {
+
+struct GemmArgs {
+  int M, N, K;
+  int k_begin, k_chunk;  // split-K: this launch's z covers [k_begin + z*k_chunk, +k_chunk)
+  const void* A; int64_t lda;
+  const void* B; int64_t ldb;
+  void* C; int64_t ldc;
+  const float* bias;
+  float alpha, beta;
+  int epi;          // bit0: exact GELU; bit1: round the branch to bf16 before the residual add
+  void* aux;        // pre-activation output (same dtype/ld as C) when GELU
+  const void* R;    // residual input (dtype/ld of C); null with beta != 0 -> C itself
+  float* partial;   // split-K fp32 slabs [z][M][N] (when non-null: raw store, no epilogue)
+};
+
+template <typename TC>
+SM_DEV void epilogue_store(const GemmArgs& g, int64_t row, int col, float acc) {
+  if (g.partial) {
+    g.partial[(int64_t)blockIdx.z * g.M * g.N + row * g.N + col] = acc;
+    return;
+  }
+  float v = g.alpha * acc;
+  if (g.bias) v += g.bias[col];
+  TC* C = (TC*)g.C;
+  const int64_t idx = row * g.ldc + col;
+  if (g.epi & 2) v = (float)(__bf16)v;   // autocast: the Linear output is bf16 before the fp32 add
+  if (g.beta != 0.f) v += g.beta * to_f<TC>(g.R ? ((const TC*)g.R)[idx] : C[idx]);
+  if (g.epi & 1) {
+    if (g.aux) ((TC*)g.aux)[idx] = from_f<TC>(v);
+    v = gelu_f(v);
+  }
+  C[idx] = from_f<TC>(v);
+}
+
+// ============================================================ bf16 MFMA kernel
+constexpr int BM = 128, BN = 128, BKT = 64;
+
+// byte offset inside a K-major [rows][64] bf16 tile (128-B rows, 16-B chunks swizzled)
+SM_DEV int kmaj_off(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+// byte offset inside an MN-major [64][128] bf16 tile (256-B rows)
+SM_DEV int mnmaj_off(int krow, int col) {
+  return krow * 256 + ((((col >> 3) ^ ((krow & 3) << 2))) << 4) + ((col & 7) << 1);
+}
+
+template <bool KMAJ>
+SM_DEV void gload_tile(const __bf16* base, int64_t ld, int rows_total, int row0, int k0, int kend,
+                       uint4 (&r)[4]) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = t + 256 * i;
+    int row, kk;
+    if (KMAJ) { row = c >> 3; kk = (c & 7) * 8; }       // [row][k] chunks
+    else      { kk = c >> 4; row = (c & 15) * 8; }      // [k][row] chunks
+    const int gr = row0 + row, gk = k0 + kk;
+    bool ok = KMAJ ? (gr < rows_total && gk < kend) : (gk < kend && gr < rows_total);
+    if (ok) {
+      const __bf16* p = KMAJ ? base + (int64_t)gr * ld + gk : base + (int64_t)gk * ld + gr;
+      r[i] = *(const uint4*)p;
+    } else {
+      r[i] = make_uint4(0, 0, 0, 0);
+    }
+  }
+}
+
+template <bool KMAJ>
+SM_DEV void lstore_tile(char* lds, const uint4 (&r)[4]) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = t + 256 * i;
+    int off;
+    if (KMAJ) off = kmaj_off(c >> 3, c & 7);
+    else      off = mnmaj_off(c >> 4, (c & 15) * 8);
+    *(uint4*)(lds + off) = r[i];
+  }
+}
+
+// Fragment for 32 rows (row base rb inside the tile) at k-substep s (16 k values).
+template <bool KMAJ>
+SM_DEV bf16x8 lread_frag(const char* lds, int rb, int s) {
+  const int l = threadIdx.x & 63;
+  if (KMAJ) {
+    const int row = rb + (l & 31);
+    const int chunk = 2 * s + (l >> 5);
+    return *(const bf16x8*)(lds + kmaj_off(row, chunk));
+  } else {
+    const int h = l >> 5, g1 = (l >> 4) & 1, i = l & 15, q = i >> 2, p = i & 3;
+    const int col = rb + 16 * g1 + 4 * p;
+    const int k0 = 16 * s + 8 * h + q;
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + mnmaj_off(k0, col)));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + mnmaj_off(k0 + 4, col)));
+    typedef __attribute__((ext_vector_type(8))) short s16x8;
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+template <bool AK, bool BK, typename TC>
+__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * BM * BKT * 2];
+  char* la = lds;
+  char* lb = lds + BM * BKT * 2;
+  // 1-D grid over (m-tile, n-tile) with an XCD-aware bijective remap: the n-tiles
+  // of one m-tile (which share the A panel) are dispatched to the same XCD's L2.
+  const int ntn = (g.N + BN - 1) / BN;
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
+  const __bf16* A = (const __bf16*)g.A;
+  const __bf16* B = (const __bf16*)g.B;
+  const int kb = g.k_begin + blockIdx.z * g.k_chunk;
+  const int ke = min(g.K, kb + g.k_chunk);
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  uint4 ra[4], rb[4];
+  if (kb < ke) {
+    gload_tile<AK>(A, g.lda, g.M, m0, kb, ke, ra);
+    gload_tile<BK>(B, g.ldb, g.N, n0, kb, ke, rb);
+  }
+  for (int k0 = kb; k0 < ke; k0 += BKT) {
+    lstore_tile<AK>(la, ra);
+    lstore_tile<BK>(lb, rb);
+    __syncthreads();
+    if (k0 + BKT < ke) {
+      gload_tile<AK>(A, g.lda, g.M, m0, k0 + BKT, ke, ra);
+      gload_tile<BK>(B, g.ldb, g.N, n0, k0 + BKT, ke, rb);
+    }
+#pragma unroll
+    for (int s = 0; s < BKT / 16; ++s) {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = lread_frag<AK>(la, wm + 32 * i, s);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfr[j] = lread_frag<BK>(lb, wn + 32 * j, s);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  const int h = l >> 5;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + wn + 32 * j + (l & 31);
+      if (col >= g.N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row < g.M) epilogue_store<TC>(g, row, col, acc[i][j][r]);
+      }
+    }
+}
+
+// ============================================================ f32 MFMA kernel
+constexpr int FBM = 64, FBN = 64, FBK = 16, FLD = 64 + 4;
+
+template <bool KMAJ>
+SM_DEV void f32_stage(const float* base, int64_t ld, int rows_total, int row0, int k0, int kend,
+                      float* lds /*[FBK][FLD]*/) {
+  const int t = threadIdx.x;
+  if (KMAJ) {                     // stored [row][k]: 64 rows x 16 k
+    const int row = t >> 2, kc = (t & 3) * 4;
+    const int gr = row0 + row;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int gk = k0 + kc + i;
+      lds[(kc + i) * FLD + row] = (gr < rows_total && gk < kend) ? base[(int64_t)gr * ld + gk] : 0.f;
+    }
+  } else {                        // stored [k][row]: 16 k x 64 rows
+    const int kr = t >> 4, rc = (t & 15) * 4;
+    const int gk = k0 + kr;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int gr = row0 + rc + i;
+      lds[kr * FLD + rc + i] = (gr < rows_total && gk < kend) ? base[(int64_t)gk * ld + gr] : 0.f;
+    }
+  }
+}
+
+template <bool AK, bool BK>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
+  __shared__ float la[FBK * FLD], lb[FBK * FLD];
+  const int ntn = (g.N + FBN - 1) / FBN;
+  const int m0 = (blockIdx.x / ntn) * FBM, n0 = (blockIdx.x % ntn) * FBN;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
+  const float* A = (const float*)g.A;
+  const float* B = (const float*)g.B;
+  const int kb = g.k_begin + blockIdx.z * g.k_chunk;
+  const int ke = min(g.K, kb + g.k_chunk);
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  for (int k0 = kb; k0 < ke; k0 += FBK) {
+    f32_stage<AK>(A, g.lda, g.M, m0, k0, ke, la);
+    f32_stage<BK>(B, g.ldb, g.N, n0, k0, ke, lb);
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < FBK / 2; ++s) {
+      const float a = la[(2 * s + (l >> 5)) * FLD + wm + (l & 31)];
+      const float b = lb[(2 * s + (l >> 5)) * FLD + wn + (l & 31)];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  const int h = l >> 5;
+  const int col = n0 + wn + (l & 31);
+  if (col < g.N) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t row = m0 + wm + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (row < g.M) epilogue_store<float>(g, row, col, acc[r]);
+    }
+  }
+}
+
+// ============================================================ split-K reduce
+template <typename TC>
+__global__ void splitk_reduce_kernel(GemmArgs g, int splits) {
+  const int64_t total = (int64_t)g.M * g.N;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int z = 0; z < splits; ++z) s += g.partial[(int64_t)z * total + i];
+    const int64_t row = i / g.N;
+    const int col = (int)(i - row * g.N);
+    GemmArgs h = g;
+    h.partial = nullptr;
+    epilogue_store<TC>(h, row, col, s);
+  }
+}
+
+int choose_splits(int M, int N, int K, bool bf16) {
+  const int bm = bf16 ? BM : FBM, bn = bf16 ? BN : FBN, bk = bf16 ? BKT : FBK;
+  const int64_t tiles = (int64_t)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+  if (tiles >= 512 || K < 4096) return 1;
+  int64_t want = (1024 + tiles - 1) / tiles;
+  int64_t max_by_k = K / (4 * bk);
+  int64_t s = want < max_by_k ? want : max_by_k;
+  if (s > 2048) s = 2048;
+  return s < 1 ? 1 : (int)s;
+}
+
+template <bool AK, bool BK>
+int launch_layout(int abt, int ct, GemmArgs g, int splits, hipStream_t st) {
+  if (abt == SM_BF16) {
+    dim3 grid(((g.N + BN - 1) / BN) * ((g.M + BM - 1) / BM), 1, splits);
+    if (ct == SM_BF16) hipLaunchKernelGGL((gemm_bf16_kernel<AK, BK, __bf16>), grid, dim3(256), 0, st, g);
+    else hipLaunchKernelGGL((gemm_bf16_kernel<AK, BK, float>), grid, dim3(256), 0, st, g);
+  } else {
+    if (ct != SM_F32) return -3;
+    dim3 grid(((g.N + FBN - 1) / FBN) * ((g.M + FBM - 1) / FBM), 1, splits);
+    hipLaunchKernelGGL((gemm_f32_kernel<AK, BK>), grid, dim3(256), 0, st, g);
+  }
+  SM_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int64_t sm_gemm_workspace_bytes(int ab_dtype, int M, int N, int K) {
+  const int s = choose_splits(M, N, K, ab_dtype == SM_BF16);
+  return s > 1 ? (int64_t)s * M * N * 4 : 0;
+}
+
+extern "C" int sm_gemm(int ab_dtype, int c_dtype, int a_layout, int b_layout, int M, int N, int K,
+                       const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc,
+                       const float* bias, float alpha, float beta, int epi, void* aux, const void* R,
+                       void* workspace, int64_t ws_bytes, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (ab_dtype == SM_BF16) {
+    if (K % 8 || lda % 8 || ldb % 8) return -2;
+    if (a_layout == 1 && M % 8) return -2;
+    if (b_layout == 1 && N % 8) return -2;
+    if (((uintptr_t)A | (uintptr_t)B) & 15) return -2;
+  }
+  GemmArgs g{};
+  g.M = M; g.N = N; g.K = K; g.A = A; g.lda = lda; g.B = B; g.ldb = ldb; g.C = C; g.ldc = ldc;
+  g.bias = bias; g.alpha = alpha; g.beta = beta; g.epi = epi; g.aux = aux; g.R = R;
+  int splits = choose_splits(M, N, K, ab_dtype == SM_BF16);
+  if (splits > 1 && (workspace == nullptr || ws_bytes < (int64_t)splits * M * N * 4)) splits = 1;
+  const int bk = ab_dtype == SM_BF16 ? BKT : FBK;
+  if (K <= 0) {  // empty reduction: C = beta*C + bias (epilogue only)
+    g.k_begin = 0; g.k_chunk = 0;
+  } else if (splits > 1) {
+    int chunk = (K + splits - 1) / splits;
+    chunk = (chunk + bk - 1) / bk * bk;
+    splits = (K + chunk - 1) / chunk;
+    g.k_begin = 0; g.k_chunk = chunk; g.partial = (float*)workspace;
+  } else {
+    g.k_begin = 0; g.k_chunk = K;
+  }
+  int rc;
+  if (a_layout == 0 && b_layout == 0) rc = launch_layout<true, true>(ab_dtype, c_dtype, g, splits, stream);
+  else if (a_layout == 0 && b_layout == 1) rc = launch_layout<true, false>(ab_dtype, c_dtype, g, splits, stream);
+  else if (a_layout == 1 && b_layout == 0) rc = launch_layout<false, true>(ab_dtype, c_dtype, g, splits, stream);
+  else rc = launch_layout<false, false>(ab_dtype, c_dtype, g, splits, stream);
+  if (rc) return rc;
+  if (splits > 1) {
+    const int64_t total = (int64_t)M * N;
+    int blocks = (int)((total + 255) / 256);
+    if (blocks > 4096) blocks = 4096;
+    if (c_dtype == SM_BF16) hipLaunchKernelGGL(splitk_reduce_kernel<__bf16>, dim3(blocks), dim3(256), 0, stream, g, splits);
+    else hipLaunchKernelGGL(splitk_reduce_kernel<float>, dim3(blocks), dim3(256), 0, stream, g, splits);
+    SM_CHECK_LAUNCH();
+  }
+  return 0;
+}

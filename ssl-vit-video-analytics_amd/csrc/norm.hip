@@ -1,0 +1,609 @@
+// Normalisation and elementwise kernels, token-major ([rows][C], NHWC) layout.
+//
+// LayerNorm (tiny_vit.py:112,115; decoder norm1/norm2/decoder_norm):
+//   one wave per row, two-pass mean/var in registers, eps 1e-5; saves mean/rstd.
+//   Backward: dx per row; dgamma/dbeta as per-block partial slabs + a column
+//   reduce (deterministic, no atomics).
+// BatchNorm2d in train mode (tiny_vit.py:16, Conv2d_BN): per-channel batch
+//   statistics over N*H*W rows: shifted fp32 partial sums per block, fp64 finalize
+//   (also the running-stat momentum update with the unbiased variance), apply with
+//   an optional fused exact GELU.  Backward recomputes x_hat (and the GELU input)
+//   from the saved pre-BN tensor, so only the conv output is kept.
+#include "common.h"
+#include "sm_api.h"
+
+namespace {
+
+// ============================================================ LayerNorm
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const TI* x, const float* g, const float* b, TO* y,
+                                                     float* mean, float* rstd, int64_t M, int C, float eps) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int l = threadIdx.x & 63;
+  if (row >= M) return;
+  const TI* xr = x + row * C;
+  constexpr int MAXV = 4;  // chunks of 4 per lane: C <= 64*4*4 = 1024
+  float v[MAXV][4];
+  float s = 0.f;
+  const int nch = C / 4;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int ci = l + 64 * i;
+    if (ci < nch) {
+      load4(xr + ci * 4, v[i]);
+      s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
+    }
+  }
+  const float mu = wave_sum(s) / C;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int ci = l + 64 * i;
+    if (ci < nch)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { const float d = v[i][j] - mu; ss += d * d; }
+  }
+  const float var = wave_sum(ss) / C;
+  const float rs = rsqrtf(var + eps);
+  TO* yr = y + row * C;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int ci = l + 64 * i;
+    if (ci < nch) {
+      float o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = ci * 4 + j;
+        o[j] = (v[i][j] - mu) * rs * g[c] + b[c];
+      }
+      store4(yr + ci * 4, o);
+    }
+  }
+  if (l == 0) { mean[row] = mu; rstd[row] = rs; }
+}
+
+// dx and per-block partial dgamma/dbeta.  Block = 4 waves, ROWS rows per block.
+template <typename TI, typename TD, typename TX>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* dy, const TI* x, const float* mean,
+                                                     const float* rstd, const float* g, TX* dx,
+                                                     float* part_g, float* part_b, int64_t M, int C,
+                                                     int rows_per_block, const TX* dres) {
+  constexpr int MAXV = 4;
+  __shared__ float red_g[4][1024], red_b[4][1024];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int nch = C / 4;
+  float ag[MAXV][4], ab[MAXV][4];
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { ag[i][j] = 0.f; ab[i][j] = 0.f; }
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  for (int rr = w; rr < rows_per_block; rr += 4) {
+    const int64_t row = r0 + rr;
+    if (row >= M) break;
+    const float mu = mean[row], rs = rstd[row];
+    float xh[MAXV][4], gg[MAXV][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int ci = l + 64 * i;
+      if (ci < nch) {
+        float xv[4], dv[4];
+        load4(x + row * C + ci * 4, xv);
+        load4(dy + row * C + ci * 4, dv);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int c = ci * 4 + j;
+          xh[i][j] = (xv[j] - mu) * rs;
+          gg[i][j] = dv[j] * g[c];
+          s1 += gg[i][j];
+          s2 += gg[i][j] * xh[i][j];
+          ag[i][j] += dv[j] * xh[i][j];
+          ab[i][j] += dv[j];
+        }
+      }
+    }
+    s1 = wave_sum(s1) / C;
+    s2 = wave_sum(s2) / C;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int ci = l + 64 * i;
+      if (ci < nch) {
+        float o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = rs * (gg[i][j] - s1 - xh[i][j] * s2);
+        TX* p = dx + row * C + ci * 4;
+        if (dres) {
+          float prev[4];
+          load4(dres + row * C + ci * 4, prev);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] += prev[j];
+        }
+        store4(p, o);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int ci = l + 64 * i;
+    if (ci < nch)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { red_g[w][ci * 4 + j] = ag[i][j]; red_b[w][ci * 4 + j] = ab[i][j]; }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    part_g[(int64_t)blockIdx.x * C + c] = red_g[0][c] + red_g[1][c] + red_g[2][c] + red_g[3][c];
+    part_b[(int64_t)blockIdx.x * C + c] = red_b[0][c] + red_b[1][c] + red_b[2][c] + red_b[3][c];
+  }
+}
+
+// out[c] (+)= sum_b part[b][c]   (fp64 accumulation; one thread per column)
+__global__ void colsum_kernel(const float* part, int nb, int C, float* out, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0;
+  for (int b = 0; b < nb; ++b) s += part[(int64_t)b * C + c];
+  out[c] = accumulate ? out[c] + (float)s : (float)s;
+}
+
+// ============================================================ BatchNorm (train)
+// Thread layout shared by the column-reduction kernels: thread t owns the 4-wide
+// channel chunk t % (C/4) and rows r = t / (C/4) (mod rows-per-pass).
+struct ColMap {
+  int nch, rpp, chunk, r;
+  SM_DEV ColMap(int C) {
+    nch = C / 4;
+    rpp = 256 / nch;
+    if (rpp < 1) rpp = 1;
+    chunk = threadIdx.x % nch;
+    r = threadIdx.x / nch;
+  }
+  SM_DEV bool active() const { return r < rpp && chunk < nch; }
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void bn_stats_kernel(const T* x, int64_t M, int C, int rows_per_block,
+                                                       float* part /*[nb][2][C]*/) {
+  __shared__ float red[2][256 * 4];
+  ColMap cm(C);
+  float s[4] = {0, 0, 0, 0}, q[4] = {0, 0, 0, 0};
+  float shift[4];
+  load4(x + cm.chunk * 4, shift);   // per-channel shift = first row (robust variance)
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
+  if (cm.active()) {
+    for (int64_t row = r0 + cm.r; row < r1; row += cm.rpp) {
+      float v[4];
+      load4(x + row * C + cm.chunk * 4, v);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { const float d = v[j] - shift[j]; s[j] += d; q[j] += d * d; }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { red[0][threadIdx.x * 4 + j] = s[j]; red[1][threadIdx.x * 4 + j] = q[j]; }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const int ch = c / 4, j = c % 4;
+    float a = 0.f, b = 0.f;
+    for (int rr = 0; rr < cm.rpp; ++rr) {
+      const int t = rr * cm.nch + ch;
+      a += red[0][t * 4 + j];
+      b += red[1][t * 4 + j];
+    }
+    part[((int64_t)blockIdx.x * 2 + 0) * C + c] = a;
+    part[((int64_t)blockIdx.x * 2 + 1) * C + c] = b;
+  }
+}
+
+template <typename T>
+__global__ void bn_finalize_kernel(const float* part, int nb, const T* x, int64_t M, int C, float eps,
+                                   float momentum, float* mean_out, float* rstd_out, float* run_mean,
+                                   float* run_var, int updates) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int b = 0; b < nb; ++b) {
+    s += part[((int64_t)b * 2 + 0) * C + c];
+    q += part[((int64_t)b * 2 + 1) * C + c];
+  }
+  const double shift = (double)to_f<T>(x[c]);
+  const double md = s / (double)M;
+  double var = q / (double)M - md * md;
+  if (var < 0) var = 0;
+  const double mean = shift + md;
+  mean_out[c] = (float)mean;
+  rstd_out[c] = (float)(1.0 / sqrt(var + (double)eps));
+  if (run_mean) {
+    const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    float rm = run_mean[c], rv = run_var[c];
+    for (int u = 0; u < updates; ++u) {
+      rm = (1.f - momentum) * rm + momentum * (float)mean;
+      rv = (1.f - momentum) * rv + momentum * (float)unb;
+    }
+    run_mean[c] = rm;
+    run_var[c] = rv;
+  }
+}
+
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void bn_apply_kernel(const TI* x, const float* mean, const float* rstd,
+                                                       const float* w, const float* b, TO* y,
+                                                       int64_t total8, int C, int gelu, const TO* R) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total8;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = i * 8;
+    const int c0 = (int)(e % C);
+    float v[8];
+    load8(x + e, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + j;
+      float t = (v[j] - mean[c]) * rstd[c] * w[c] + b[c];
+      v[j] = gelu ? gelu_f(t) : t;
+    }
+    if (R) {
+      float r[8];
+      load8(R + e, r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += r[j];
+    }
+    store8(y + e, v);
+  }
+}
+
+// per-channel sums of g and g*x_hat where g = dy (* gelu'(bn(x)) when gelu)
+template <typename TI, typename TD>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const TD* dy, const TI* x, const float* mean,
+                                                            const float* rstd, const float* w, const float* b,
+                                                            int64_t M, int C, int rows_per_block, int gelu,
+                                                            float* part) {
+  __shared__ float red[2][256 * 4];
+  ColMap cm(C);
+  float sg[4] = {0, 0, 0, 0}, sgx[4] = {0, 0, 0, 0};
+  float mu[4], rs[4], ww[4], bb[4];
+  if (cm.active()) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = cm.chunk * 4 + j;
+      mu[j] = mean[c]; rs[j] = rstd[c]; ww[j] = w[c]; bb[j] = b[c];
+    }
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t r1 = min(M, r0 + rows_per_block);
+    for (int64_t row = r0 + cm.r; row < r1; row += cm.rpp) {
+      float xv[4], dv[4];
+      load4(x + row * C + cm.chunk * 4, xv);
+      load4(dy + row * C + cm.chunk * 4, dv);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float xh = (xv[j] - mu[j]) * rs[j];
+        float gg = dv[j];
+        if (gelu) gg *= gelu_grad(xh * ww[j] + bb[j]);
+        sg[j] += gg;
+        sgx[j] += gg * xh;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { red[0][threadIdx.x * 4 + j] = sg[j]; red[1][threadIdx.x * 4 + j] = sgx[j]; }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const int ch = c / 4, j = c % 4;
+    float a = 0.f, bsum = 0.f;
+    for (int rr = 0; rr < cm.rpp; ++rr) {
+      const int t = rr * cm.nch + ch;
+      a += red[0][t * 4 + j];
+      bsum += red[1][t * 4 + j];
+    }
+    part[((int64_t)blockIdx.x * 2 + 0) * C + c] = a;
+    part[((int64_t)blockIdx.x * 2 + 1) * C + c] = bsum;
+  }
+}
+
+// sums -> dgamma (+=), dbeta (+=), and the two per-channel coefficients for dx
+__global__ void bn_bwd_finalize_kernel(const float* part, int nb, int64_t M, int C, float* dw, float* db,
+                                       float* coef /*[2][C]: mean(g), mean(g*xhat)*/) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double a = 0.0, b = 0.0;
+  for (int k = 0; k < nb; ++k) {
+    a += part[((int64_t)k * 2 + 0) * C + c];
+    b += part[((int64_t)k * 2 + 1) * C + c];
+  }
+  if (dw) dw[c] += (float)b;
+  if (db) db[c] += (float)a;
+  coef[c] = (float)(a / (double)M);
+  coef[C + c] = (float)(b / (double)M);
+}
+
+template <typename TI, typename TD, typename TX>
+__global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const TD* dy, const TI* x, const float* mean,
+                                                        const float* rstd, const float* w, const float* b,
+                                                        const float* coef, TX* dx, int64_t total8, int C,
+                                                        int gelu) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total8;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = i * 8;
+    const int c0 = (int)(e % C);
+    float xv[8], dv[8], o[8];
+    load8(x + e, xv);
+    load8(dy + e, dv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + j;
+      const float xh = (xv[j] - mean[c]) * rstd[c];
+      float gg = dv[j];
+      if (gelu) gg *= gelu_grad(xh * w[c] + b[c]);
+      o[j] = w[c] * rstd[c] * (gg - coef[c] - xh * coef[C + c]);
+    }
+    store8(dx + e, o);
+  }
+}
+
+// ============================================================ elementwise
+template <typename T, typename TG>
+__global__ void gelu_bwd_kernel(const T* pre, const TG* dy, TG* dx, int64_t total8) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total8;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float p[8], d[8];
+    load8(pre + i * 8, p);
+    load8(dy + i * 8, d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] *= gelu_grad(p[j]);
+    store8(dx + i * 8, d);
+  }
+}
+
+template <typename TA, typename TB, typename TO>
+__global__ void add_kernel(const TA* a, const TB* b, TO* o, int64_t total8) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total8;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float x[8], y[8];
+    load8(a + i * 8, x);
+    load8(b + i * 8, y);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] += y[j];
+    store8(o + i * 8, x);
+  }
+}
+
+template <typename TA, typename TO>
+__global__ void cast_kernel(const TA* a, TO* o, int64_t total8) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total8;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float x[8];
+    load8(a + i * 8, x);
+    store8(o + i * 8, x);
+  }
+}
+
+template <typename T>
+__global__ void gelu_fwd_kernel(const T* x, T* y, int64_t total8) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total8;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float v[8];
+    load8(x + i * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = gelu_f(v[j]);
+    store8(y + i * 8, v);
+  }
+}
+
+// per-block column partial sums of x [M][C]
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_part_kernel(const T* x, int64_t M, int C, int rows_per_block,
+                                                          float* part) {
+  __shared__ float red[256 * 4];
+  ColMap cm(C);
+  float s[4] = {0, 0, 0, 0};
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
+  if (cm.active())
+    for (int64_t row = r0 + cm.r; row < r1; row += cm.rpp) {
+      float v[4];
+      load4(x + row * C + cm.chunk * 4, v);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s[j] += v[j];
+    }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) red[threadIdx.x * 4 + j] = s[j];
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const int ch = c / 4, j = c % 4;
+    float a = 0.f;
+    for (int rr = 0; rr < cm.rpp; ++rr) a += red[(rr * cm.nch + ch) * 4 + j];
+    part[(int64_t)blockIdx.x * C + c] = a;
+  }
+}
+
+inline int ew_blocks(int64_t n8) {
+  int64_t b = (n8 + 255) / 256;
+  if (b > 8192) b = 8192;
+  return b < 1 ? 1 : (int)b;
+}
+inline int red_rows_per_block(int64_t M, int C) {
+  // aim for ~2048 blocks, at least 64 rows each
+  int64_t r = (M + 2047) / 2048;
+  if (r < 64) r = 64;
+  return (int)r;
+}
+
+}  // namespace
+
+#define DISPATCH2(DT1, DT2, ...)                                                           \
+  do {                                                                                   \
+    if ((DT1) == SM_F32 && (DT2) == SM_F32) { typedef float T1; typedef float T2; __VA_ARGS__; }     \
+    else if ((DT1) == SM_F32 && (DT2) == SM_BF16) { typedef float T1; typedef __bf16 T2; __VA_ARGS__; } \
+    else if ((DT1) == SM_BF16 && (DT2) == SM_F32) { typedef __bf16 T1; typedef float T2; __VA_ARGS__; } \
+    else { typedef __bf16 T1; typedef __bf16 T2; __VA_ARGS__; }                          \
+  } while (0)
+
+extern "C" int sm_layernorm_fwd(int x_dtype, int y_dtype, int64_t M, int C, const void* x, const float* gamma,
+                                const float* beta, void* y, float* mean, float* rstd, float eps,
+                                hipStream_t st) {
+  if (M <= 0) return 0;
+  if (C % 4 || C > 1024) return -2;
+  const int blocks = (int)((M + 3) / 4);
+  DISPATCH2(x_dtype, y_dtype,
+            hipLaunchKernelGGL((ln_fwd_kernel<T1, T2>), dim3(blocks), dim3(256), 0, st, (const T1*)x, gamma,
+                               beta, (T2*)y, mean, rstd, M, C, eps));
+  SM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int64_t sm_layernorm_bwd_workspace_bytes(int64_t M, int C) {
+  const int64_t rpb = 64;
+  const int64_t nb = (M + rpb - 1) / rpb;
+  return nb * C * 4 * 2;
+}
+
+// dx (+)= LN backward; dgamma/dbeta (+)= (accumulated into the fp32 grad sinks)
+extern "C" int sm_layernorm_bwd(int x_dtype, int dy_dtype, int dx_dtype, int64_t M, int C, const void* dy,
+                                const void* x, const float* mean, const float* rstd, const float* gamma,
+                                void* dx, const void* dres, float* dgamma, float* dbeta, void* ws,
+                                int64_t ws_bytes, hipStream_t st) {
+  if (M <= 0) return 0;
+  if (C % 4 || C > 1024) return -2;
+  const int rpb = 64;
+  const int nb = (int)((M + rpb - 1) / rpb);
+  if (ws_bytes < (int64_t)nb * C * 8) return -4;
+  float* pg = (float*)ws;
+  float* pb = pg + (int64_t)nb * C;
+  if (x_dtype != dx_dtype) return -3;   // dx has the dtype of the LN input stream
+  DISPATCH2(x_dtype, dy_dtype,
+            hipLaunchKernelGGL((ln_bwd_kernel<T1, T2, T1>), dim3(nb), dim3(256), 0, st, (const T2*)dy,
+                               (const T1*)x, mean, rstd, gamma, (T1*)dx, pg, pb, M, C, rpb, (const T1*)dres));
+  SM_CHECK_LAUNCH();
+  hipLaunchKernelGGL(colsum_kernel, dim3((C + 255) / 256), dim3(256), 0, st, pg, nb, C, dgamma, 1);
+  hipLaunchKernelGGL(colsum_kernel, dim3((C + 255) / 256), dim3(256), 0, st, pb, nb, C, dbeta, 1);
+  SM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int64_t sm_bn_workspace_bytes(int64_t M, int C) {
+  const int64_t rpb = red_rows_per_block(M, C);
+  const int64_t nb = (M + rpb - 1) / rpb;
+  return nb * 2 * C * 4 + 2 * C * 4;
+}
+
+// batch statistics -> mean/rstd (+ running-stat update `updates` times)
+extern "C" int sm_bn_stats(int x_dtype, int64_t M, int C, const void* x, float* mean, float* rstd,
+                           float* run_mean, float* run_var, float momentum, float eps, int updates, void* ws,
+                           int64_t ws_bytes, hipStream_t st) {
+  if (M <= 0) return -2;
+  if (C % 4 || C / 4 > 256) return -2;
+  const int rpb = red_rows_per_block(M, C);
+  const int nb = (int)((M + rpb - 1) / rpb);
+  if (ws_bytes < (int64_t)nb * 2 * C * 4) return -4;
+  float* part = (float*)ws;
+  if (x_dtype == SM_BF16) {
+    hipLaunchKernelGGL(bn_stats_kernel<__bf16>, dim3(nb), dim3(256), 0, st, (const __bf16*)x, M, C, rpb, part);
+    hipLaunchKernelGGL(bn_finalize_kernel<__bf16>, dim3((C + 127) / 128), dim3(128), 0, st, part, nb,
+                       (const __bf16*)x, M, C, eps, momentum, mean, rstd, run_mean, run_var, updates);
+  } else {
+    hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(nb), dim3(256), 0, st, (const float*)x, M, C, rpb, part);
+    hipLaunchKernelGGL(bn_finalize_kernel<float>, dim3((C + 127) / 128), dim3(128), 0, st, part, nb,
+                       (const float*)x, M, C, eps, momentum, mean, rstd, run_mean, run_var, updates);
+  }
+  SM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int sm_bn_apply(int x_dtype, int y_dtype, int64_t M, int C, const void* x, const float* mean,
+                           const float* rstd, const float* w, const float* b, void* y, int gelu,
+                           const void* R, hipStream_t st) {
+  if (M <= 0) return 0;
+  if (C % 8) return -2;
+  const int64_t n8 = M * C / 8;
+  DISPATCH2(x_dtype, y_dtype,
+            hipLaunchKernelGGL((bn_apply_kernel<T1, T2>), dim3(ew_blocks(n8)), dim3(256), 0, st, (const T1*)x,
+                               mean, rstd, w, b, (T2*)y, n8, C, gelu, (const T2*)R));
+  SM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int sm_bn_bwd(int x_dtype, int g_dtype, int64_t M, int C, const void* dy, const void* x,
+                         const float* mean, const float* rstd, const float* w, const float* b, int gelu,
+                         void* dx, float* dw, float* db, void* ws, int64_t ws_bytes, hipStream_t st) {
+  if (M <= 0) return 0;
+  if (C % 8 || C / 4 > 256) return -2;
+  const int rpb = red_rows_per_block(M, C);
+  const int nb = (int)((M + rpb - 1) / rpb);
+  if (ws_bytes < (int64_t)nb * 2 * C * 4 + 2 * C * 4) return -4;
+  float* part = (float*)ws;
+  float* coef = part + (int64_t)nb * 2 * C;
+  DISPATCH2(x_dtype, g_dtype,
+            hipLaunchKernelGGL((bn_bwd_reduce_kernel<T1, T2>), dim3(nb), dim3(256), 0, st, (const T2*)dy,
+                               (const T1*)x, mean, rstd, w, b, M, C, rpb, gelu, part));
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 127) / 128), dim3(128), 0, st, part, nb, M, C, dw, db, coef);
+  const int64_t n8 = M * C / 8;
+  DISPATCH2(x_dtype, g_dtype,
+            hipLaunchKernelGGL((bn_bwd_dx_kernel<T1, T2, T2>), dim3(ew_blocks(n8)), dim3(256), 0, st,
+                               (const T2*)dy, (const T1*)x, mean, rstd, w, b, coef, (T2*)dx, n8, C, gelu));
+  SM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int sm_gelu_bwd(int pre_dtype, int g_dtype, int64_t n, const void* pre, const void* dy, void* dx,
+                           hipStream_t st) {
+  if (n <= 0) return 0;
+  if (n % 8) return -2;
+  DISPATCH2(pre_dtype, g_dtype,
+            hipLaunchKernelGGL((gelu_bwd_kernel<T1, T2>), dim3(ew_blocks(n / 8)), dim3(256), 0, st,
+                               (const T1*)pre, (const T2*)dy, (T2*)dx, n / 8));
+  SM_CHECK_LAUNCH();
+  return 0;
+}
+
+// o = a + b  (a: a_dtype, b/o: o_dtype)
+extern "C" int sm_add(int a_dtype, int o_dtype, int64_t n, const void* a, const void* b, void* o, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (n % 8) return -2;
+  DISPATCH2(a_dtype, o_dtype,
+            hipLaunchKernelGGL((add_kernel<T1, T2, T2>), dim3(ew_blocks(n / 8)), dim3(256), 0, st, (const T1*)a,
+                               (const T2*)b, (T2*)o, n / 8));
+  SM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int sm_cast(int a_dtype, int o_dtype, int64_t n, const void* a, void* o, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (n % 8) return -2;
+  DISPATCH2(a_dtype, o_dtype,
+            hipLaunchKernelGGL((cast_kernel<T1, T2>), dim3(ew_blocks(n / 8)), dim3(256), 0, st, (const T1*)a,
+                               (T2*)o, n / 8));
+  SM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int64_t sm_colsum_workspace_bytes(int64_t M, int C) {
+  const int64_t rpb = red_rows_per_block(M, C);
+  return ((M + rpb - 1) / rpb) * C * 4;
+}
+
+// out[c] (+)= sum_m x[m][c]   (bias gradients)
+extern "C" int sm_colsum(int dtype, int64_t M, int C, const void* x, float* out, int accumulate, void* ws,
+                         int64_t ws_bytes, hipStream_t st) {
+  if (M <= 0) return 0;
+  if (C % 4 || C / 4 > 256) return -2;
+  const int rpb = red_rows_per_block(M, C);
+  const int nb = (int)((M + rpb - 1) / rpb);
+  if (ws_bytes < (int64_t)nb * C * 4) return -4;
+  if (dtype == SM_BF16)
+    hipLaunchKernelGGL(colsum_part_kernel<__bf16>, dim3(nb), dim3(256), 0, st, (const __bf16*)x, M, C, rpb, (float*)ws);
+  else
+    hipLaunchKernelGGL(colsum_part_kernel<float>, dim3(nb), dim3(256), 0, st, (const float*)x, M, C, rpb, (float*)ws);
+  hipLaunchKernelGGL(colsum_kernel, dim3((C + 255) / 256), dim3(256), 0, st, (const float*)ws, nb, C, out, accumulate);
+  SM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int sm_gelu_fwd(int dtype, int64_t n, const void* x, void* y, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (n % 8) return -2;
+  if (dtype == SM_BF16)
+    hipLaunchKernelGGL(gelu_fwd_kernel<__bf16>, dim3(ew_blocks(n / 8)), dim3(256), 0, st, (const __bf16*)x, (__bf16*)y, n / 8);
+  else
+    hipLaunchKernelGGL(gelu_fwd_kernel<float>, dim3(ew_blocks(n / 8)), dim3(256), 0, st, (const float*)x, (float*)y, n / 8);
+  SM_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,67 @@
+"""Compile csrc/*.hip into libsslmae.so for gfx950 (hipcc, in-tree, no JIT cache).
+
+The objects are rebuilt only when a source or header is newer than the library.
+"""
+import glob
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+ROOT_PKG = os.path.dirname(PKG_DIR)
+CSRC = os.path.join(ROOT_PKG, "csrc")
+REPO = os.path.dirname(ROOT_PKG)
+INCLUDE = os.path.join(REPO, "include")
+LIB = os.path.join(PKG_DIR, "libsslmae.so")
+BUILD = os.path.join(ROOT_PKG, "build")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("SM_OFFLOAD_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", CSRC, "-I", INCLUDE,
+         "-Wno-unused-result", "-munsafe-fp-atomics"]
+
+
+def _sources():
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+
+
+def _newest_input():
+    files = _sources() + glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(INCLUDE, "*.h"))
+    return max(os.path.getmtime(f) for f in files)
+
+
+def needs_build():
+    return not os.path.exists(LIB) or os.path.getmtime(LIB) < _newest_input()
+
+
+def build(verbose=False, jobs=None):
+    if not needs_build():
+        return LIB
+    os.makedirs(BUILD, exist_ok=True)
+    srcs = _sources()
+    objs = [os.path.join(BUILD, os.path.basename(s) + ".o") for s in srcs]
+
+    def compile_one(pair):
+        src, obj = pair
+        cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-6000:]}")
+        if verbose:
+            print("compiled", os.path.basename(src), file=sys.stderr)
+        return obj
+
+    jobs = jobs or min(len(srcs), max(1, (os.cpu_count() or 2) // 2), 8)
+    with ThreadPoolExecutor(jobs) as ex:
+        list(ex.map(compile_one, zip(srcs, objs)))
+    tmp = LIB + ".tmp"
+    cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", tmp] + objs
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(verbose=True))

@@ -1,0 +1,349 @@
+"""Thin tensor-level wrappers over the C ABI (include/sm_api.h).
+
+Each function allocates its outputs (torch caching allocator, current device),
+launches on the current stream and returns tensors.  No CPU path exists: a
+missing library or a non-CUDA tensor raises.
+"""
+import math
+
+import torch
+
+from . import _lib
+from ._lib import call, dt, ptr, query, stream
+
+
+def _chk(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise _lib.KernelError("ssl_mae_amd kernels need device tensors (no CPU fallback)")
+
+
+def _ws(nbytes, device):
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+
+
+# ------------------------------------------------------------------ GEMM
+def gemm(A, B, C, M, N, K, a_layout, b_layout, lda, ldb, ldc, bias=None, alpha=1.0, beta=0.0,
+         gelu=False, aux=None, R=None, round_branch=False):
+    _chk(A, B, C)
+    ab = dt(A)
+    if dt(B) != ab:
+        raise _lib.KernelError("GEMM operands must share a dtype")
+    nbytes = query("sm_gemm_workspace_bytes", ab, M, N, K)
+    ws = _ws(nbytes, A.device) if nbytes else None
+    epi = (1 if gelu else 0) | (2 if round_branch else 0)
+    call("sm_gemm", ab, dt(C), a_layout, b_layout, M, N, K, ptr(A), lda, ptr(B), ldb, ptr(C), ldc, ptr(bias),
+         float(alpha), float(beta), epi, ptr(aux), ptr(R), ptr(ws), nbytes, stream())
+    return C
+
+
+def linear(x, w, bias=None, out_dtype=None, gelu=False, residual=None, round_branch=False):
+    """y = x @ w^T + bias (+ residual) (GELU optional, returns (y, pre) then)."""
+    M, K = x.shape
+    N = w.shape[0]
+    out = torch.empty((M, N), dtype=out_dtype or x.dtype, device=x.device)
+    pre = torch.empty_like(out) if gelu else None
+    gemm(x, w, out, M, N, K, 0, 0, K, K, N, bias=bias, gelu=gelu, aux=pre,
+         beta=1.0 if residual is not None else 0.0, R=residual, round_branch=round_branch)
+    return (out, pre) if gelu else out
+
+
+def linear_dx(dy, w, out_dtype=None, residual=None):
+    """dx = dy @ w (+ residual);  dy [M,N], w [N,K]."""
+    M, N = dy.shape
+    K = w.shape[1]
+    out = torch.empty((M, K), dtype=out_dtype or dy.dtype, device=dy.device)
+    gemm(dy, w, out, M, K, N, 0, 1, N, K, K, beta=1.0 if residual is not None else 0.0, R=residual)
+    return out
+
+
+def linear_dw(dy, x, grad_sink):
+    """grad_sink[N,K] += dy^T @ x   (fp32 sink)."""
+    M, N = dy.shape
+    K = x.shape[1]
+    gemm(dy, x, grad_sink, N, K, M, 1, 1, N, K, K, beta=1.0)
+    return grad_sink
+
+
+def colsum(x, out, accumulate=True):
+    M, C = x.shape
+    nbytes = query("sm_colsum_workspace_bytes", M, C)
+    ws = _ws(nbytes, x.device)
+    call("sm_colsum", dt(x), M, C, ptr(x), ptr(out), 1 if accumulate else 0, ptr(ws), nbytes, stream())
+    return out
+
+
+# ------------------------------------------------------------------ attention
+def attn_fwd(qkv, N, L, H, D, drop_p=0.0, seed=0):
+    _chk(qkv)
+    out = torch.empty((N * L, H * D), dtype=qkv.dtype, device=qkv.device)
+    lse = torch.empty((N, H, L), dtype=torch.float32, device=qkv.device)
+    call("sm_attn_fwd", dt(qkv), N, L, H, D, ptr(qkv), ptr(out), ptr(lse), 1.0 / math.sqrt(D), float(drop_p),
+         int(seed), stream())
+    return out, lse
+
+
+def attn_bwd(qkv, o, do, lse, N, L, H, D, drop_p=0.0, seed=0):
+    _chk(qkv, o, do, lse)
+    dqkv = torch.empty_like(qkv)
+    delta = torch.empty((N, H, L), dtype=torch.float32, device=qkv.device)
+    call("sm_attn_bwd", dt(qkv), N, L, H, D, ptr(qkv), ptr(o), ptr(do), ptr(lse), ptr(delta), ptr(dqkv),
+         1.0 / math.sqrt(D), float(drop_p), int(seed), stream())
+    return dqkv
+
+
+# ------------------------------------------------------------------ LayerNorm
+def layernorm(x, gamma, beta, out_dtype=None, eps=1e-5):
+    _chk(x)
+    M, C = x.shape
+    y = torch.empty((M, C), dtype=out_dtype or x.dtype, device=x.device)
+    mean = torch.empty(M, dtype=torch.float32, device=x.device)
+    rstd = torch.empty(M, dtype=torch.float32, device=x.device)
+    call("sm_layernorm_fwd", dt(x), dt(y), M, C, ptr(x), ptr(gamma), ptr(beta), ptr(y), ptr(mean), ptr(rstd),
+         float(eps), stream())
+    return y, mean, rstd
+
+
+def layernorm_recompute(x, gamma, beta, out_dtype, eps=1e-5):
+    return layernorm(x, gamma, beta, out_dtype, eps)[0]
+
+
+def layernorm_bwd(dy, x, mean, rstd, gamma, dgamma, dbeta, dres=None):
+    M, C = x.shape
+    dx = torch.empty_like(x)
+    nbytes = query("sm_layernorm_bwd_workspace_bytes", M, C)
+    ws = _ws(nbytes, x.device)
+    call("sm_layernorm_bwd", dt(x), dt(dy), dt(dx), M, C, ptr(dy), ptr(x), ptr(mean), ptr(rstd), ptr(gamma),
+         ptr(dx), ptr(dres), ptr(dgamma), ptr(dbeta), ptr(ws), nbytes, stream())
+    return dx
+
+
+# ------------------------------------------------------------------ BatchNorm (train)
+def bn_stats(x2d, running_mean=None, running_var=None, momentum=0.1, eps=1e-5, updates=1):
+    _chk(x2d)
+    M, C = x2d.shape
+    mean = torch.empty(C, dtype=torch.float32, device=x2d.device)
+    rstd = torch.empty(C, dtype=torch.float32, device=x2d.device)
+    nbytes = query("sm_bn_workspace_bytes", M, C)
+    ws = _ws(nbytes, x2d.device)
+    call("sm_bn_stats", dt(x2d), M, C, ptr(x2d), ptr(mean), ptr(rstd), ptr(running_mean), ptr(running_var),
+         float(momentum), float(eps), int(updates), ptr(ws), nbytes, stream())
+    return mean, rstd
+
+
+def bn_apply(x2d, mean, rstd, w, b, gelu=False, out_dtype=None, residual=None):
+    M, C = x2d.shape
+    y = torch.empty((M, C), dtype=out_dtype or x2d.dtype, device=x2d.device)
+    call("sm_bn_apply", dt(x2d), dt(y), M, C, ptr(x2d), ptr(mean), ptr(rstd), ptr(w), ptr(b), ptr(y),
+         1 if gelu else 0, ptr(residual), stream())
+    return y
+
+
+def bn_bwd(dy, x2d, mean, rstd, w, b, gelu, dw_sink, db_sink):
+    M, C = x2d.shape
+    dx = torch.empty_like(dy)
+    nbytes = query("sm_bn_workspace_bytes", M, C)
+    ws = _ws(nbytes, x2d.device)
+    call("sm_bn_bwd", dt(x2d), dt(dy), M, C, ptr(dy), ptr(x2d), ptr(mean), ptr(rstd), ptr(w), ptr(b),
+         1 if gelu else 0, ptr(dx), ptr(dw_sink), ptr(db_sink), ptr(ws), nbytes, stream())
+    return dx
+
+
+# ------------------------------------------------------------------ elementwise
+def gelu(x):
+    y = torch.empty_like(x)
+    call("sm_gelu_fwd", dt(x), x.numel(), ptr(x), ptr(y), stream())
+    return y
+
+
+def gelu_bwd(pre, dy):
+    dx = torch.empty_like(dy)
+    call("sm_gelu_bwd", dt(pre), dt(dy), dy.numel(), ptr(pre), ptr(dy), ptr(dx), stream())
+    return dx
+
+
+def add(a, b, out_dtype=None):
+    o = torch.empty(b.shape, dtype=out_dtype or b.dtype, device=b.device)
+    if dt(b) != dt(o):
+        raise _lib.KernelError("add: b and out must share dtype")
+    call("sm_add", dt(a), dt(o), o.numel(), ptr(a), ptr(b), ptr(o), stream())
+    return o
+
+
+def cast(a, dtype, out=None):
+    o = out if out is not None else torch.empty(a.shape, dtype=dtype, device=a.device)
+    call("sm_cast", dt(a), dt(o), a.numel(), ptr(a), ptr(o), stream())
+    return o
+
+
+def fill_(t, v):
+    call("sm_fill", ptr(t), t.numel(), float(v), stream())
+    return t
+
+
+# ------------------------------------------------------------------ convolutions
+def stem_im2col(clip, out_dtype, frames_view=None):
+    """clip [B,3,T,H,W] (fp32, any strides) -> col [B*T*Ho*Wo, 32] (stride 2, pad 1)."""
+    _chk(clip)
+    if clip.dtype != torch.float32:
+        clip = clip.float()
+    if clip.dim() == 5:
+        B, C, T, H, W = clip.shape
+        sB, sC, sT, sH, sW = clip.stride()
+    else:  # frames [N,3,H,W]
+        B, C, H, W = clip.shape
+        T = 1
+        sB, sC, sH, sW = clip.stride()
+        sT = 0
+    Ho, Wo = (H + 1) // 2, (W + 1) // 2
+    col = torch.empty((B * T * Ho * Wo, 32), dtype=out_dtype, device=clip.device)
+    call("sm_stem_im2col", dt(col), ptr(clip), B, T, H, W, sB, sC, sT, sH, sW, 2, ptr(col), stream())
+    return col, (B * T, Ho, Wo)
+
+
+def im2col3(x, F, H, W, C, stride):
+    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    col = torch.empty((F * Ho * Wo, 9 * C), dtype=x.dtype, device=x.device)
+    call("sm_im2col3", dt(x), ptr(x), F, H, W, C, stride, ptr(col), stream())
+    return col
+
+
+def col2im3(dcol, F, H, W, C, stride):
+    dx = torch.empty((F * H * W, C), dtype=dcol.dtype, device=dcol.device)
+    call("sm_col2im3", dt(dcol), ptr(dcol), F, H, W, C, stride, ptr(dx), stream())
+    return dx
+
+
+def conv_wpack(w, Kpad, order, dtype):
+    Cout, Cin = w.shape[0], w.shape[1]
+    out = torch.empty((Cout, Kpad), dtype=dtype, device=w.device)
+    call("sm_conv_wpack", dt(out), ptr(w), ptr(out), Cout, Cin, Kpad, order, stream())
+    return out
+
+
+def conv_wunpack_add(packed, grad, order):
+    Cout, Cin = grad.shape[0], grad.shape[1]
+    call("sm_conv_wunpack_add", ptr(packed), ptr(grad), Cout, Cin, packed.shape[1], order, stream())
+
+
+def dwconv(x, w, F, H, W, C, stride):
+    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    y = torch.empty((F * Ho * Wo, C), dtype=x.dtype, device=x.device)
+    call("sm_dwconv_fwd", dt(x), ptr(x), ptr(w), ptr(y), F, H, W, C, stride, stream())
+    return y
+
+
+def dwconv_bwd(dy, x, w, dw_sink, F, H, W, C, stride, need_dx=True):
+    dx = torch.empty_like(x) if need_dx else None
+    nbytes = query("sm_dwconv_wgrad_workspace_bytes", F, H, W, C, stride)
+    ws = _ws(nbytes, x.device)
+    call("sm_dwconv_bwd", dt(x), ptr(dy), ptr(x), ptr(w), ptr(dx), ptr(dw_sink), F, H, W, C, stride, ptr(ws),
+         nbytes, stream())
+    return dx
+
+
+def se_fwd(x, F, HW, C, w1, w2):
+    R = w1.shape[0]
+    dev = x.device
+    pooled = torch.empty((F, C), dtype=torch.float32, device=dev)
+    h1 = torch.empty((F, R), dtype=torch.float32, device=dev)
+    s = torch.empty((F, C), dtype=torch.float32, device=dev)
+    y = torch.empty_like(x)
+    call("sm_se_fwd", dt(x), ptr(x), F, HW, C, R, ptr(w1), ptr(w2), ptr(pooled), ptr(h1), ptr(s), ptr(y), stream())
+    return y, pooled, h1, s
+
+
+def se_scale(x, s, F, HW, C):
+    y = torch.empty_like(x)
+    call("sm_se_scale", dt(x), ptr(x), ptr(s), ptr(y), F, HW, C, stream())
+    return y
+
+
+def se_bwd(dy, x, F, HW, C, w1, w2, s, h1):
+    R = w1.shape[0]
+    dev = x.device
+    ds = torch.empty((F, C), dtype=torch.float32, device=dev)
+    dz2 = torch.empty((F, C), dtype=torch.float32, device=dev)
+    dz1 = torch.empty((F, R), dtype=torch.float32, device=dev)
+    dpool = torch.empty((F, C), dtype=torch.float32, device=dev)
+    dx = torch.empty_like(x)
+    call("sm_se_bwd", dt(x), ptr(dy), ptr(x), F, HW, C, R, ptr(w1), ptr(w2), ptr(s), ptr(h1), ptr(ds), ptr(dz2),
+         ptr(dz1), ptr(dpool), ptr(dx), stream())
+    return dx, dz2, dz1
+
+
+# ------------------------------------------------------------------ MAE glue
+def tube_mask(noise, T, n_mask, with_index=True):
+    """noise [B,L] fp32 (device) -> mask uint8 [B,T,L], idx int32 [B*T*n_mask]."""
+    _chk(noise)
+    B, L = noise.shape
+    mask = torch.empty((B, T, L), dtype=torch.uint8, device=noise.device)
+    idx = torch.empty((B * T * n_mask,), dtype=torch.int32, device=noise.device) if with_index else None
+    call("sm_tube_mask", ptr(noise), B, T, L, n_mask, ptr(mask), ptr(idx), stream())
+    return mask, idx
+
+
+def pos_blend(y, tpos, spos, tok, mask_u8, B, T, L, D, out_dtype):
+    x = torch.empty((B * T * L, D), dtype=out_dtype, device=y.device)
+    call("sm_pos_blend_fwd", dt(y), dt(x), ptr(y), ptr(tpos), ptr(spos), ptr(tok), ptr(mask_u8), ptr(x), B, T, L, D,
+         stream())
+    return x
+
+
+def pos_blend_bwd(dx, mask_u8, y_dtype, dtpos, dspos, dtok, B, T, L, D):
+    dy = torch.empty(dx.shape, dtype=y_dtype, device=dx.device)
+    ws = torch.empty((2, B * T, D), dtype=torch.float32, device=dx.device)
+    call("sm_pos_blend_bwd", dt(dx), dt(dy), ptr(dx), ptr(mask_u8), ptr(dy), ptr(dtpos), ptr(dspos), ptr(dtok),
+         ptr(ws), B, T, L, D, stream())
+    return dy
+
+
+def _clip_args(clip):
+    B, C, T, H, W = clip.shape
+    return (B, T, H, W) + tuple(clip.stride())
+
+
+def mae_loss_fwd(pred, clip, mask_u8, norm_pix=True):
+    _chk(pred, clip, mask_u8)
+    B, T, H, W, sB, sC, sT, sH, sW = _clip_args(clip)
+    L = (H // 8) * (W // 8)
+    loss = torch.empty((), dtype=torch.float32, device=pred.device)
+    denom = torch.empty((1,), dtype=torch.float32, device=pred.device)
+    nbytes = query("sm_loss_workspace_bytes", B, T, L)
+    ws = _ws(nbytes, pred.device)
+    call("sm_mae_loss_fwd", dt(pred), ptr(pred), ptr(clip), sB, sC, sT, sH, sW, ptr(mask_u8), B, T, H, W,
+         1 if norm_pix else 0, ptr(loss), ptr(denom), ptr(ws), nbytes, stream())
+    return loss, denom
+
+
+def mae_loss_bwd(pred, clip, mask_u8, norm_pix, grad_out, denom):
+    B, T, H, W, sB, sC, sT, sH, sW = _clip_args(clip)
+    dpred = torch.empty_like(pred)
+    g = grad_out.reshape(1).float().contiguous()
+    call("sm_mae_loss_bwd", dt(pred), ptr(pred), ptr(clip), sB, sC, sT, sH, sW, ptr(mask_u8), B, T, H, W,
+         1 if norm_pix else 0, ptr(g), ptr(denom), ptr(dpred), stream())
+    return dpred
+
+
+def gather_rows(src2d, idx):
+    out = torch.empty((idx.numel(), src2d.shape[1]), dtype=src2d.dtype, device=src2d.device)
+    call("sm_gather_rows", dt(src2d), ptr(src2d), ptr(idx), idx.numel(), src2d.shape[1], ptr(out), stream())
+    return out
+
+
+def std(x):
+    out = torch.empty((), dtype=torch.float32, device=x.device)
+    nbytes = query("sm_std_workspace_bytes")
+    ws = _ws(nbytes, x.device)
+    call("sm_std", dt(x), ptr(x), x.numel(), ptr(out), ptr(ws), nbytes, stream())
+    return out
+
+
+# ------------------------------------------------------------------ optimizer
+def nonfinite(g, flag):
+    call("sm_nonfinite", ptr(g), g.numel(), ptr(flag), stream())
+
+
+def adamw(p, g, m, v, lr, b1, b2, eps, wd, found_inf, step, shadow=None):
+    call("sm_adamw", ptr(p), ptr(g), ptr(m), ptr(v), ptr(shadow), p.numel(), float(lr), float(b1), float(b2),
+         float(eps), float(wd), ptr(found_inf), ptr(step), stream())

@@ -1,0 +1,400 @@
+"""Kernel-level parity on the GPU: every C-ABI entry point against a plain fp32
+CPU reference of the same op (torch CPU ops / the oracle).  Tolerances: f32 mode
+1e-4-ish relative (exact-fp32 MFMA, different summation order); bf16 mode
+compared with the fp32 reference of the SAME bf16-rounded inputs, 2e-2 of scale.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from ssl_mae_amd import _lib as L
+    L.load()
+
+
+def KK():
+    from ssl_mae_amd import kernels
+    return kernels
+
+
+def rel_err(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-12)).item()
+
+
+TOL = {torch.float32: 2e-5, torch.bfloat16: 2e-2}
+
+
+def rnd(*shape, dtype=torch.float32, scale=1.0, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(dtype)
+
+
+# ------------------------------------------------------------------ GEMM
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("la,lb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,N,K", [(200, 72, 96), (1000, 384, 192), (64, 1152, 384), (256, 96, 8)])
+def test_gemm_layouts(dtype, la, lb, M, N, K):
+    A = rnd(M, K, dtype=dtype, seed=1)
+    Bm = rnd(K, N, dtype=dtype, seed=2)
+    ref = A.float() @ Bm.float()
+    a_st = A if la == 0 else A.t().contiguous()        # [M][K] or [K][M]
+    b_st = Bm.t().contiguous() if lb == 0 else Bm       # [N][K] or [K][N]
+    C = torch.empty(M, N, dtype=dtype, device=DEV)
+    KK().gemm(a_st.to(DEV), b_st.to(DEV), C, M, N, K, la, lb, a_st.shape[1], b_st.shape[1], N)
+    assert rel_err(C, ref) < TOL[dtype] * (4 if dtype == torch.float32 else 1)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_epilogues(dtype):
+    M, N, Kd = 300, 192, 128
+    x = rnd(M, Kd, dtype=dtype, seed=3)
+    w = rnd(N, Kd, dtype=dtype, seed=4, scale=0.1)
+    b = rnd(N, seed=5)
+    r = rnd(M, N, dtype=dtype, seed=6)
+    kk = KK()
+    y = kk.linear(x.to(DEV), w.to(DEV), b.to(DEV), residual=r.to(DEV))
+    ref = x.float() @ w.float().t() + b + r.float()
+    assert rel_err(y, ref) < TOL[dtype]
+    y, pre = kk.linear(x.to(DEV), w.to(DEV), b.to(DEV), gelu=True)
+    refp = x.float() @ w.float().t() + b
+    assert rel_err(pre, refp) < TOL[dtype]
+    assert rel_err(y, F.gelu(refp)) < TOL[dtype]
+
+
+def test_gemm_round_branch_residual_fp32():
+    M, N, Kd = 128, 384, 384
+    x = rnd(M, Kd, dtype=torch.bfloat16, seed=7)
+    w = rnd(N, Kd, dtype=torch.bfloat16, seed=8, scale=0.05)
+    b = rnd(N, seed=9)
+    r = rnd(M, N, seed=10)
+    y = KK().linear(x.to(DEV), w.to(DEV), b.to(DEV), out_dtype=torch.float32, residual=r.to(DEV), round_branch=True)
+    ref = (x.float() @ w.float().t() + b).bfloat16().float() + r
+    assert rel_err(y, ref) < 1e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_splitk_dw(dtype):
+    M, N, Kd = 70000, 96, 384   # dW of a 1x1 conv: reduction over 70k rows -> split-K
+    dy = rnd(M, N, dtype=dtype, seed=11, scale=0.1)
+    x = rnd(M, Kd, dtype=dtype, seed=12)
+    sink = torch.zeros(N, Kd, device=DEV)
+    KK().linear_dw(dy.to(DEV), x.to(DEV), sink)
+    ref = dy.float().t() @ x.float()
+    assert rel_err(sink, ref) < (1e-4 if dtype == torch.float32 else 2e-2)
+
+
+def test_colsum():
+    x = rnd(5000, 384, seed=13)
+    out = torch.ones(384, device=DEV)
+    KK().colsum(x.to(DEV), out, accumulate=True)
+    assert rel_err(out, x.sum(0) + 1) < 1e-5
+
+
+# ------------------------------------------------------------------ attention
+def _attn_ref(qkv, N, L, H, D):
+    qkv = qkv.float().reshape(N, L, 3, H, D).permute(2, 0, 3, 1, 4)
+    q, k, v = [t.detach().clone().requires_grad_(True) for t in qkv]
+    o = F.scaled_dot_product_attention(q, k, v)
+    return q, k, v, o
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("D", [32, 64])
+@pytest.mark.parametrize("L", [50, 128, 200])
+def test_attention_fwd_bwd(dtype, D, L):
+    N, H = 2, 3
+    qkv = rnd(N * L, 3 * H * D, dtype=dtype, seed=20 + L + D)
+    dO = rnd(N * L, H * D, dtype=dtype, seed=21 + L + D)
+    q, k, v, o_ref = _attn_ref(qkv, N, L, H, D)
+    o_ref_flat = o_ref.transpose(1, 2).reshape(N * L, H * D)
+    o_ref_flat.backward(dO.float())
+    dqkv_ref = torch.stack([q.grad, k.grad, v.grad]).permute(1, 3, 0, 2, 4).reshape(N * L, 3 * H * D)
+    kk = KK()
+    o, lse = kk.attn_fwd(qkv.to(DEV), N, L, H, D)
+    assert rel_err(o, o_ref_flat) < TOL[dtype]
+    s = (q.detach() @ k.detach().transpose(-1, -2)) / math.sqrt(D)
+    lse_ref = torch.logsumexp(s, -1)
+    assert rel_err(lse, lse_ref) < (1e-5 if dtype == torch.float32 else 2e-2)
+    dqkv = kk.attn_bwd(qkv.to(DEV), o, dO.to(DEV), lse, N, L, H, D)
+    assert rel_err(dqkv, dqkv_ref) < (1e-4 if dtype == torch.float32 else 3e-2)
+
+
+def test_attention_dropout_statistics():
+    """Dropout on P: E[O] unchanged; the same seed gives the same output."""
+    N, L, H, D = 1, 256, 2, 64
+    qkv = rnd(N * L, 3 * H * D, dtype=torch.bfloat16, seed=30).to(DEV)
+    kk = KK()
+    o0, _ = kk.attn_fwd(qkv, N, L, H, D)
+    outs = [kk.attn_fwd(qkv, N, L, H, D, drop_p=0.1, seed=s)[0].float() for s in range(64)]
+    again = kk.attn_fwd(qkv, N, L, H, D, drop_p=0.1, seed=0)[0].float()
+    assert torch.equal(outs[0], again)
+    mean = torch.stack(outs).mean(0)
+    assert rel_err(mean, o0.float()) < 0.1
+
+
+# ------------------------------------------------------------------ LayerNorm
+@pytest.mark.parametrize("xd,yd", [(torch.float32, torch.float32), (torch.bfloat16, torch.bfloat16),
+                                   (torch.float32, torch.bfloat16)])
+@pytest.mark.parametrize("C", [192, 384])
+def test_layernorm(xd, yd, C):
+    M = 777
+    x = (rnd(M, C, seed=40) * 3 + 1).to(xd)
+    g = rnd(C, seed=41) * 0.1 + 1
+    b = rnd(C, seed=42) * 0.1
+    dy = rnd(M, C, seed=43).to(yd)
+    xr = x.float().requires_grad_(True)
+    gr = g.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    yr = F.layer_norm(xr, (C,), gr, br, 1e-5)
+    yr.backward(dy.float())
+    kk = KK()
+    y, mean, rstd = kk.layernorm(x.to(DEV), g.to(DEV), b.to(DEV), out_dtype=yd)
+    tol = 2e-5 if yd == torch.float32 else 1e-2
+    assert rel_err(y, yr) < tol
+    dg = torch.zeros(C, device=DEV)
+    db = torch.zeros(C, device=DEV)
+    res = rnd(M, C, seed=44).to(xd)
+    dx = kk.layernorm_bwd(dy.to(DEV), x.to(DEV), mean, rstd, g.to(DEV), dg, db, dres=res.to(DEV))
+    tol = 1e-4 if xd == torch.float32 and yd == torch.float32 else 2e-2
+    assert rel_err(dx, xr.grad + res.float()) < tol
+    assert rel_err(dg, gr.grad) < 1e-4
+    assert rel_err(db, br.grad) < 1e-4
+
+
+# ------------------------------------------------------------------ BatchNorm
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("C", [48, 96, 384, 768])
+@pytest.mark.parametrize("gelu", [False, True])
+def test_batchnorm_train(dtype, C, gelu):
+    M = 3000
+    x = (rnd(M, C, seed=50) * 2 + 0.5).to(dtype)
+    w = rnd(C, seed=51) * 0.1 + 1
+    b = rnd(C, seed=52) * 0.1
+    dy = rnd(M, C, seed=53).to(dtype)
+    xr = x.float().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    rm_ref = torch.zeros(C)
+    rv_ref = torch.ones(C)
+    yr = F.batch_norm(xr, rm_ref, rv_ref, wr, br, True, 0.1, 1e-5)
+    if gelu:
+        yr = F.gelu(yr)
+    yr.backward(dy.float())
+    kk = KK()
+    rm = torch.zeros(C, device=DEV)
+    rv = torch.ones(C, device=DEV)
+    xd = x.to(DEV)
+    mean, rstd = kk.bn_stats(xd, rm, rv)
+    assert rel_err(rm, rm_ref) < 1e-4 and rel_err(rv, rv_ref) < 1e-4
+    y = kk.bn_apply(xd, mean, rstd, w.to(DEV), b.to(DEV), gelu=gelu)
+    assert rel_err(y, yr) < TOL[dtype] * 2
+    dw = torch.zeros(C, device=DEV)
+    db = torch.zeros(C, device=DEV)
+    dx = kk.bn_bwd(dy.to(DEV), xd, mean, rstd, w.to(DEV), b.to(DEV), gelu, dw, db)
+    assert rel_err(dx, xr.grad) < (1e-4 if dtype == torch.float32 else 3e-2)
+    assert rel_err(dw, wr.grad) < (1e-4 if dtype == torch.float32 else 2e-2)
+    assert rel_err(db, br.grad) < 1e-4
+
+
+# ------------------------------------------------------------------ convs
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("stride", [1, 2])
+def test_dwconv(dtype, stride):
+    Fn, H, W, C = 3, 14, 12, 64
+    x = rnd(Fn, H, W, C, dtype=dtype, seed=60)
+    w = rnd(C, 1, 3, 3, seed=61) * 0.3
+    xr = x.float().permute(0, 3, 1, 2).contiguous().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    yr = F.conv2d(xr, wr, None, stride, 1, 1, C)
+    dy = rnd(*yr.shape, seed=62).to(dtype).float()
+    yr.backward(dy)
+    kk = KK()
+    y = kk.dwconv(x.to(DEV).reshape(-1, C), w.to(DEV).reshape(C, 9), Fn, H, W, C, stride)
+    assert rel_err(y, yr.permute(0, 2, 3, 1).reshape(-1, C)) < TOL[dtype]
+    dw = torch.zeros(C, 9, device=DEV)
+    dyd = dy.permute(0, 2, 3, 1).reshape(-1, C).to(dtype).to(DEV)
+    dx = kk.dwconv_bwd(dyd, x.to(DEV).reshape(-1, C), w.to(DEV).reshape(C, 9), dw, Fn, H, W, C, stride)
+    assert rel_err(dx, xr.grad.permute(0, 2, 3, 1).reshape(-1, C)) < TOL[dtype]
+    assert rel_err(dw, wr.grad.reshape(C, 9)) < (1e-4 if dtype == torch.float32 else 2e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_stem_conv_via_im2col(dtype):
+    B, T, S = 2, 3, 32
+    clip = rnd(B, 3, T, S, S, seed=70)
+    w1 = rnd(48, 3, 3, 3, seed=71) * 0.2
+    kk = KK()
+    col, (Fn, Ho, Wo) = kk.stem_im2col(clip.to(DEV), dtype)
+    w1p = kk.conv_wpack(w1.to(DEV), 32, 0, dtype)
+    y = kk.linear(col, w1p)
+    frames = clip.permute(0, 2, 1, 3, 4).reshape(B * T, 3, S, S)
+    ref = F.conv2d(frames.to(dtype).float(), w1, None, 2, 1).permute(0, 2, 3, 1).reshape(-1, 48)
+    assert rel_err(y, ref) < TOL[dtype] * 2
+    # conv2 48->96 k3 s1 via im2col3 + GEMM, and its dgrad via col2im3
+    x2 = rnd(Fn, Ho, Wo, 48, dtype=dtype, seed=72)
+    w2 = rnd(96, 48, 3, 3, seed=73) * 0.05
+    col2 = kk.im2col3(x2.to(DEV).reshape(-1, 48), Fn, Ho, Wo, 48, 1)
+    w2p = kk.conv_wpack(w2.to(DEV), 432, 1, dtype)
+    y2 = kk.linear(col2, w2p)
+    xr = x2.float().permute(0, 3, 1, 2).contiguous().requires_grad_(True)
+    wr = w2.clone().requires_grad_(True)
+    ref2 = F.conv2d(xr, wr, None, 1, 1)
+    assert rel_err(y2, ref2.permute(0, 2, 3, 1).reshape(-1, 96)) < TOL[dtype] * 2
+    dy = rnd(*ref2.shape, seed=74).to(dtype).float()
+    ref2.backward(dy)
+    dyd = dy.permute(0, 2, 3, 1).reshape(-1, 96).to(dtype).to(DEV)
+    dcol = kk.linear_dx(dyd, w2p)
+    dx = kk.col2im3(dcol, Fn, Ho, Wo, 48, 1)
+    assert rel_err(dx, xr.grad.permute(0, 2, 3, 1).reshape(-1, 48)) < TOL[dtype] * 2
+    dwp = torch.zeros(96, 432, device=DEV)
+    kk.linear_dw(dyd, col2, dwp)
+    g = torch.zeros(96, 48, 3, 3, device=DEV)
+    kk.conv_wunpack_add(dwp, g, 1)
+    assert rel_err(g, wr.grad) < (1e-4 if dtype == torch.float32 else 2e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_se_layer(dtype):
+    Fn, HW, C = 4, 49, 96
+    R = C // 4
+    x = rnd(Fn, HW, C, dtype=dtype, seed=80)
+    w1 = rnd(R, C, seed=81) * 0.2
+    w2 = rnd(C, R, seed=82) * 0.2
+    xr = x.float().requires_grad_(True)
+    w1r = w1.clone().requires_grad_(True)
+    w2r = w2.clone().requires_grad_(True)
+    p = xr.mean(1)
+    h = torch.relu(p @ w1r.t())
+    s = torch.sigmoid(h @ w2r.t())
+    yr = xr * s[:, None, :]
+    dy = rnd(Fn, HW, C, seed=83).to(dtype).float()
+    yr.backward(dy)
+    kk = KK()
+    y, pooled, h1, sd = kk.se_fwd(x.to(DEV).reshape(-1, C), Fn, HW, C, w1.to(DEV), w2.to(DEV))
+    assert rel_err(y, yr.reshape(-1, C)) < TOL[dtype]
+    dx, dz2, dz1 = kk.se_bwd(dy.to(dtype).to(DEV).reshape(-1, C), x.to(DEV).reshape(-1, C), Fn, HW, C,
+                             w1.to(DEV), w2.to(DEV), sd, h1)
+    assert rel_err(dx, xr.grad.reshape(-1, C)) < TOL[dtype] * 2
+    dw2 = torch.zeros(C, R, device=DEV)
+    KK().gemm(dz2, h1, dw2, C, R, Fn, 1, 1, C, R, R, beta=1.0)
+    dw1 = torch.zeros(R, C, device=DEV)
+    KK().gemm(dz1, pooled, dw1, R, C, Fn, 1, 1, R, C, C, beta=1.0)
+    assert rel_err(dw2, w2r.grad) < (1e-4 if dtype == torch.float32 else 2e-2)
+    assert rel_err(dw1, w1r.grad) < (1e-4 if dtype == torch.float32 else 2e-2)
+
+
+# ------------------------------------------------------------------ MAE glue
+def test_tube_mask_and_gather_bit_exact():
+    from oracle import mae_oracle as O
+    B, T, L, r = 16, 8, 784, 0.75
+    n_mask = int(r * L)
+    torch.manual_seed(7)
+    ref = O.get_tube_mask(B, T, L, r)
+    torch.manual_seed(7)
+    noise = torch.stack([torch.rand(L) for _ in range(B)])
+    mask, idx = KK().tube_mask(noise.to(DEV), T, n_mask)
+    assert torch.equal(mask.cpu().bool(), ref)
+    ref_idx = torch.nonzero(ref.reshape(-1)).reshape(-1).int()
+    assert torch.equal(idx.cpu(), ref_idx)
+    pred = rnd(B * T * L, 192, dtype=torch.bfloat16, seed=90)
+    g = KK().gather_rows(pred.to(DEV), idx)
+    assert torch.equal(g.cpu(), pred[ref.reshape(-1)])
+    sd = KK().std(g)
+    assert abs(sd.item() - pred[ref.reshape(-1)].float().std().item()) < 1e-4
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_mae_loss(dtype):
+    from oracle import mae_oracle as O
+    B, T, S = 2, 3, 32
+    L = (S // 8) ** 2
+    clip = rnd(B, 3, T, S, S, seed=100)
+    torch.manual_seed(3)
+    mask = O.get_tube_mask(B, T, L, 0.75)
+    pred = rnd(B, T * L, 192, dtype=dtype, seed=101)
+    pr = pred.float().requires_grad_(True)
+    tgt = O.norm_pix(O.patchify(clip, 8))
+    lr_ = O.masked_mse(pr, tgt, mask)
+    lr_.backward()
+    kk = KK()
+    m8 = mask.to(torch.uint8).to(DEV)
+    loss, denom = kk.mae_loss_fwd(pred.to(DEV), clip.to(DEV), m8)
+    assert abs(loss.item() - lr_.item()) < 1e-5 * max(1, abs(lr_.item()))
+    g = torch.ones((), device=DEV)
+    dpred = kk.mae_loss_bwd(pred.to(DEV), clip.to(DEV), m8, True, g, denom)
+    assert rel_err(dpred, pr.grad) < (1e-5 if dtype == torch.float32 else 1e-2)
+
+
+def test_pos_blend():
+    B, T, L, D = 2, 3, 16, 384
+    y = rnd(B * T * L, D, dtype=torch.bfloat16, seed=110)
+    tpos = rnd(1, T, 1, D, seed=111) * 0.02
+    spos = rnd(1, 1, L, D, seed=112) * 0.02
+    tok = rnd(1, 1, D, seed=113) * 0.02
+    torch.manual_seed(0)
+    mask = torch.rand(B, T, L) < 0.5
+    yr = y.float().requires_grad_(True)
+    tr = tpos.clone().requires_grad_(True)
+    sr = spos.clone().requires_grad_(True)
+    kr = tok.clone().requires_grad_(True)
+    x = yr.reshape(B, T, L, D) + (tr + sr)
+    m = mask.float()[..., None]
+    x = x * (1 - m) + kr * m
+    dx = rnd(B, T, L, D, seed=114)
+    x.backward(dx)
+    kk = KK()
+    m8 = mask.to(torch.uint8).to(DEV)
+    out = kk.pos_blend(y.to(DEV), tpos.to(DEV).reshape(T, D), spos.to(DEV).reshape(L, D), tok.to(DEV).reshape(D),
+                       m8, B, T, L, D, torch.float32)
+    assert rel_err(out, x.reshape(-1, D)) < 1e-6
+    dt_ = torch.zeros(T, D, device=DEV)
+    ds_ = torch.zeros(L, D, device=DEV)
+    dk_ = torch.zeros(D, device=DEV)
+    dy = kk.pos_blend_bwd(dx.reshape(-1, D).to(DEV), m8, torch.bfloat16, dt_, ds_, dk_, B, T, L, D)
+    assert rel_err(dy, yr.grad.reshape(-1, D)) < 1e-2
+    assert rel_err(dt_, tr.grad.reshape(T, D)) < 1e-5
+    assert rel_err(ds_, sr.grad.reshape(L, D)) < 1e-5
+    assert rel_err(dk_, kr.grad.reshape(D)) < 1e-5
+
+
+def test_adamw_matches_torch():
+    n = 10000
+    p0 = rnd(n, seed=120)
+    grads = [rnd(n, seed=121 + i) * 0.01 for i in range(3)]
+    pr = p0.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([pr], lr=5e-4, weight_decay=0.05)
+    for g in grads:
+        pr.grad = g.clone()
+        opt.step()
+    kk = KK()
+    p = p0.to(DEV)
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    flag = torch.zeros(1, dtype=torch.int32, device=DEV)
+    step = torch.zeros(1, dtype=torch.int64, device=DEV)
+    for g in grads:
+        gd = g.to(DEV)
+        flag.zero_()
+        kk.nonfinite(gd, flag)
+        kk.adamw(p, gd, m, v, 5e-4, 0.9, 0.999, 1e-8, 0.05, flag, step)
+    assert rel_err(p, pr.detach()) < 1e-6
+    bad = grads[0].clone().to(DEV)
+    bad[5] = float("nan")
+    flag.zero_()
+    kk.nonfinite(bad, flag)
+    before = p.clone()
+    kk.adamw(p, bad, m, v, 5e-4, 0.9, 0.999, 1e-8, 0.05, flag, step)
+    assert torch.equal(p, before) and step.item() == 3
