@@ -58,8 +58,8 @@ int sm_layernorm_bwd(int x_dtype, int dy_dtype, int dx_dtype, int64_t M, int C, 
 /* ---- BatchNorm2d, train mode (tiny_vit.py:16 Conv2d_BN), channels-last [M][C] */
 int64_t sm_bn_workspace_bytes(int64_t M, int C);
 int sm_bn_stats(int x_dtype, int64_t M, int C, const void* x, float* mean, float* rstd,
-                float* run_mean, float* run_var, float momentum, float eps, int updates, void* ws,
-                int64_t ws_bytes, hipStream_t st);
+                float* run_mean, float* run_var, int64_t* num_batches_tracked, float momentum, float eps,
+                int updates, void* ws, int64_t ws_bytes, hipStream_t st);
 int sm_bn_apply(int x_dtype, int y_dtype, int64_t M, int C, const void* x, const float* mean,
                 const float* rstd, const float* w, const float* b, void* y, int gelu, const void* R,
                 hipStream_t st);
@@ -121,6 +121,9 @@ int sm_mae_loss_fwd(int pred_dtype, const void* pred, const float* clip, int64_t
 int sm_mae_loss_bwd(int pred_dtype, const void* pred, const float* clip, int64_t sB, int64_t sC,
                     int64_t sT, int64_t sH, int64_t sW, const uint8_t* mask, int B, int T, int H, int W,
                     int norm_pix, const float* grad_out, const float* denom, void* dpred, hipStream_t st);
+int sm_patchify(const float* imgs, int B, int C, int T, int H, int W, int64_t sB, int64_t sC, int64_t sT,
+                int64_t sH, int64_t sW, int p, float* out, hipStream_t st);
+int sm_unpatchify(const float* tokens, int B, int C, int T, int H, int W, int p, float* imgs, hipStream_t st);
 int sm_gather_rows(int dtype, const void* src, const int32_t* idx, int64_t nrows, int C, void* dst,
                    hipStream_t st);
 int64_t sm_std_workspace_bytes(void);
@@ -128,9 +131,11 @@ int sm_std(int dtype, const void* x, int64_t n, float* out, void* ws, int64_t ws
 
 /* ---- optimizer (train_ssl_mae.py:163 AdamW, :87-89 GradScaler inf-skip) */
 int sm_nonfinite(const float* g, int64_t n, int* flag, hipStream_t st);
+/* p *= a (data-parallel gradient averaging after a SUM all-reduce) */
+int sm_scale(float* p, int64_t n, float a, hipStream_t st);
 int sm_adamw(float* p, const float* g, float* m, float* v, void* bf16_shadow, int64_t n, float lr,
              float b1, float b2, float eps, float wd, const int* found_inf, int64_t* step,
-             hipStream_t st);
+             int advance_step, hipStream_t st);
 
 #ifdef __cplusplus
 }

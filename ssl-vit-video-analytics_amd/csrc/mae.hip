@@ -315,6 +315,33 @@ __global__ void fill_kernel(float* p, int64_t n, float v) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
 }
 
+// imgs [B][C][T][H][W] (strided) <-> tokens [B][T*hp*wp][p*p*C], feature (pi,qi,c)
+__global__ void patchify_kernel(const float* x, int64_t sB, int64_t sC, int64_t sT, int64_t sH, int64_t sW, int B,
+                                int C, int T, int H, int W, int p, float* out, int inverse) {
+  const int hp = H / p, wp = W / p;
+  const int F = p * p * C;
+  const int64_t total = (int64_t)B * T * hp * wp * F;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int f = (int)(i % F);
+    int64_t tok = i / F;
+    const int w = (int)(tok % wp);
+    tok /= wp;
+    const int h = (int)(tok % hp);
+    tok /= hp;
+    const int t = (int)(tok % T);
+    const int b = (int)(tok / T);
+    const int c = f % C, qi = (f / C) % p, pi = f / (C * p);
+    const int64_t src = b * sB + c * sC + t * sT + (int64_t)(h * p + pi) * sH + (int64_t)(w * p + qi) * sW;
+    if (inverse) out[src] = x[i];
+    else out[i] = x[src];
+  }
+}
+
+__global__ void scale_kernel(float* p, int64_t n, float a) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    p[i] *= a;
+}
+
 inline int ew_blocks(int64_t n) {
   int64_t b = (n + 255) / 256;
   if (b > 8192) b = 8192;
@@ -453,11 +480,11 @@ extern "C" int sm_nonfinite(const float* g, int64_t n, int* flag, hipStream_t st
 
 extern "C" int sm_adamw(float* p, const float* g, float* m, float* v, void* bf16_shadow, int64_t n, float lr,
                         float b1, float b2, float eps, float wd, const int* found_inf, int64_t* step,
-                        hipStream_t st) {
-  if (n <= 0) return 0;
-  hipLaunchKernelGGL(adamw_kernel, dim3(ew_blocks(n)), dim3(256), 0, st, p, g, m, v, (__bf16*)bf16_shadow, n, lr, b1,
-                     b2, eps, wd, found_inf, step);
-  hipLaunchKernelGGL(step_incr_kernel, dim3(1), dim3(1), 0, st, found_inf, step);
+                        int advance_step, hipStream_t st) {
+  if (n > 0)
+    hipLaunchKernelGGL(adamw_kernel, dim3(ew_blocks(n)), dim3(256), 0, st, p, g, m, v, (__bf16*)bf16_shadow, n, lr,
+                       b1, b2, eps, wd, found_inf, step);
+  if (advance_step) hipLaunchKernelGGL(step_incr_kernel, dim3(1), dim3(1), 0, st, found_inf, step);
   SM_CHECK_LAUNCH();
   return 0;
 }
@@ -465,6 +492,38 @@ extern "C" int sm_adamw(float* p, const float* g, float* m, float* v, void* bf16
 extern "C" int sm_fill(float* p, int64_t n, float v, hipStream_t st) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(fill_kernel, dim3(ew_blocks(n)), dim3(256), 0, st, p, n, v);
+  SM_CHECK_LAUNCH();
+  return 0;
+}
+
+// patchify (train_ssl_mae.py:26-31): imgs [B,C,T,H,W] fp32 (strides) -> out [B, T*hp*wp, p*p*C]
+extern "C" int sm_patchify(const float* imgs, int B, int C, int T, int H, int W, int64_t sB, int64_t sC, int64_t sT,
+                           int64_t sH, int64_t sW, int p, float* out, hipStream_t st) {
+  if (p <= 0 || H % p || W % p) return -2;
+  const int64_t total = (int64_t)B * C * T * H * W;
+  if (total <= 0) return 0;
+  hipLaunchKernelGGL(patchify_kernel, dim3(ew_blocks(total)), dim3(256), 0, st, imgs, sB, sC, sT, sH, sW, B, C, T, H,
+                     W, p, out, 0);
+  SM_CHECK_LAUNCH();
+  return 0;
+}
+
+// exact inverse of sm_patchify: tokens -> imgs (contiguous [B,C,T,H,W])
+extern "C" int sm_unpatchify(const float* tokens, int B, int C, int T, int H, int W, int p, float* imgs,
+                             hipStream_t st) {
+  if (p <= 0 || H % p || W % p) return -2;
+  const int64_t total = (int64_t)B * C * T * H * W;
+  if (total <= 0) return 0;
+  const int64_t sW = 1, sH = W, sT = (int64_t)H * W, sC = (int64_t)T * H * W, sB = (int64_t)C * T * H * W;
+  hipLaunchKernelGGL(patchify_kernel, dim3(ew_blocks(total)), dim3(256), 0, st, tokens, sB, sC, sT, sH, sW, B, C, T,
+                     H, W, p, imgs, 1);
+  SM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int sm_scale(float* p, int64_t n, float a, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(scale_kernel, dim3(ew_blocks(n)), dim3(256), 0, st, p, n, a);
   SM_CHECK_LAUNCH();
   return 0;
 }

@@ -198,8 +198,9 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const T* x, int64_t M, in
 template <typename T>
 __global__ void bn_finalize_kernel(const float* part, int nb, const T* x, int64_t M, int C, float eps,
                                    float momentum, float* mean_out, float* rstd_out, float* run_mean,
-                                   float* run_var, int updates) {
+                                   float* run_var, int updates, int64_t* nbt) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0 && nbt) *nbt += updates;
   if (c >= C) return;
   double s = 0.0, q = 0.0;
   for (int b = 0; b < nb; ++b) {
@@ -390,8 +391,8 @@ __global__ void gelu_fwd_kernel(const T* x, T* y, int64_t total8) {
 
 // per-block column partial sums of x [M][C]
 template <typename T>
-__global__ __launch_bounds__(256) void colsum_part_kernel(const T* x, int64_t M, int C, int rows_per_block,
-                                                          float* part) {
+__global__ __launch_bounds__(256) void colsum_part_kernel(const T* x, int64_t ld, int64_t M, int C,
+                                                          int rows_per_block, float* part) {
   __shared__ float red[256 * 4];
   ColMap cm(C);
   float s[4] = {0, 0, 0, 0};
@@ -400,7 +401,7 @@ __global__ __launch_bounds__(256) void colsum_part_kernel(const T* x, int64_t M,
   if (cm.active())
     for (int64_t row = r0 + cm.r; row < r1; row += cm.rpp) {
       float v[4];
-      load4(x + row * C + cm.chunk * 4, v);
+      load4(x + row * ld + cm.chunk * 4, v);
 #pragma unroll
       for (int j = 0; j < 4; ++j) s[j] += v[j];
     }
@@ -487,8 +488,8 @@ extern "C" int64_t sm_bn_workspace_bytes(int64_t M, int C) {
 
 // batch statistics -> mean/rstd (+ running-stat update `updates` times)
 extern "C" int sm_bn_stats(int x_dtype, int64_t M, int C, const void* x, float* mean, float* rstd,
-                           float* run_mean, float* run_var, float momentum, float eps, int updates, void* ws,
-                           int64_t ws_bytes, hipStream_t st) {
+                           float* run_mean, float* run_var, int64_t* num_batches_tracked, float momentum, float eps,
+                           int updates, void* ws, int64_t ws_bytes, hipStream_t st) {
   if (M <= 0) return -2;
   if (C % 4 || C / 4 > 256) return -2;
   const int rpb = red_rows_per_block(M, C);
@@ -498,11 +499,13 @@ extern "C" int sm_bn_stats(int x_dtype, int64_t M, int C, const void* x, float* 
   if (x_dtype == SM_BF16) {
     hipLaunchKernelGGL(bn_stats_kernel<__bf16>, dim3(nb), dim3(256), 0, st, (const __bf16*)x, M, C, rpb, part);
     hipLaunchKernelGGL(bn_finalize_kernel<__bf16>, dim3((C + 127) / 128), dim3(128), 0, st, part, nb,
-                       (const __bf16*)x, M, C, eps, momentum, mean, rstd, run_mean, run_var, updates);
+                       (const __bf16*)x, M, C, eps, momentum, mean, rstd, run_mean, run_var, updates,
+                       num_batches_tracked);
   } else {
     hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(nb), dim3(256), 0, st, (const float*)x, M, C, rpb, part);
     hipLaunchKernelGGL(bn_finalize_kernel<float>, dim3((C + 127) / 128), dim3(128), 0, st, part, nb,
-                       (const float*)x, M, C, eps, momentum, mean, rstd, run_mean, run_var, updates);
+                       (const float*)x, M, C, eps, momentum, mean, rstd, run_mean, run_var, updates,
+                       num_batches_tracked);
   }
   SM_CHECK_LAUNCH();
   return 0;
@@ -584,15 +587,24 @@ extern "C" int64_t sm_colsum_workspace_bytes(int64_t M, int C) {
 extern "C" int sm_colsum(int dtype, int64_t M, int C, const void* x, float* out, int accumulate, void* ws,
                          int64_t ws_bytes, hipStream_t st) {
   if (M <= 0) return 0;
-  if (C % 4 || C / 4 > 256) return -2;
+  if (C % 4) return -2;
   const int rpb = red_rows_per_block(M, C);
   const int nb = (int)((M + rpb - 1) / rpb);
   if (ws_bytes < (int64_t)nb * C * 4) return -4;
-  if (dtype == SM_BF16)
-    hipLaunchKernelGGL(colsum_part_kernel<__bf16>, dim3(nb), dim3(256), 0, st, (const __bf16*)x, M, C, rpb, (float*)ws);
-  else
-    hipLaunchKernelGGL(colsum_part_kernel<float>, dim3(nb), dim3(256), 0, st, (const float*)x, M, C, rpb, (float*)ws);
-  hipLaunchKernelGGL(colsum_kernel, dim3((C + 255) / 256), dim3(256), 0, st, (const float*)ws, nb, C, out, accumulate);
+  const int esz = dtype == SM_BF16 ? 2 : 4;
+  for (int c0 = 0; c0 < C; c0 += 1024) {       // 1024-column slices (ColMap covers <= 256 chunks of 4)
+    const int cs = C - c0 < 1024 ? C - c0 : 1024;
+    const char* xs = (const char*)x + (int64_t)c0 * esz;
+    float* part = (float*)ws;
+    if (dtype == SM_BF16)
+      hipLaunchKernelGGL(colsum_part_kernel<__bf16>, dim3(nb), dim3(256), 0, st, (const __bf16*)xs, (int64_t)C, M,
+                         cs, rpb, part);
+    else
+      hipLaunchKernelGGL(colsum_part_kernel<float>, dim3(nb), dim3(256), 0, st, (const float*)xs, (int64_t)C, M, cs,
+                         rpb, part);
+    hipLaunchKernelGGL(colsum_kernel, dim3((cs + 255) / 256), dim3(256), 0, st, (const float*)part, nb, cs, out + c0,
+                       accumulate);
+  }
   SM_CHECK_LAUNCH();
   return 0;
 }

@@ -35,8 +35,8 @@ _SIGS = {
     "sm_layernorm_bwd": (_c_i32, [_c_i32, _c_i32, _c_i32, _c_i64, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p,
                                   _c_p, _c_p, _c_p, _c_p, _c_i64, _c_p]),
     "sm_bn_workspace_bytes": (_c_i64, [_c_i64, _c_i32]),
-    "sm_bn_stats": (_c_i32, [_c_i32, _c_i64, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_f32, _c_i32, _c_p,
-                             _c_i64, _c_p]),
+    "sm_bn_stats": (_c_i32, [_c_i32, _c_i64, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_f32, _c_i32,
+                             _c_p, _c_i64, _c_p]),
     "sm_bn_apply": (_c_i32, [_c_i32, _c_i32, _c_i64, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_p,
                              _c_p]),
     "sm_bn_bwd": (_c_i32, [_c_i32, _c_i32, _c_i64, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_p,
@@ -72,12 +72,16 @@ _SIGS = {
                                  _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_i64, _c_p]),
     "sm_mae_loss_bwd": (_c_i32, [_c_i32, _c_p, _c_p, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_p, _c_i32, _c_i32,
                                  _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p]),
+    "sm_patchify": (_c_i32, [_c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64,
+                             _c_i32, _c_p, _c_p]),
+    "sm_unpatchify": (_c_i32, [_c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p]),
+    "sm_scale": (_c_i32, [_c_p, _c_i64, _c_f32, _c_p]),
     "sm_gather_rows": (_c_i32, [_c_i32, _c_p, _c_p, _c_i64, _c_i32, _c_p, _c_p]),
     "sm_std_workspace_bytes": (_c_i64, []),
     "sm_std": (_c_i32, [_c_i32, _c_p, _c_i64, _c_p, _c_p, _c_i64, _c_p]),
     "sm_nonfinite": (_c_i32, [_c_p, _c_i64, _c_p, _c_p]),
     "sm_adamw": (_c_i32, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i64, _c_f32, _c_f32, _c_f32, _c_f32, _c_f32, _c_p, _c_p,
-                          _c_p]),
+                          _c_i32, _c_p]),
 }
 
 _lib = None

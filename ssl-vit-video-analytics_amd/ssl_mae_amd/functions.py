@@ -1,0 +1,349 @@
+"""Autograd Functions of the MAE step: each one drives a fused group of HIP kernels
+forward and backward (the "engine" of this framework).
+
+Activations are token-major (channels-last): [rows][C].  Each Function saves
+only what its backward cannot cheaply recompute (pre-BN conv outputs, attention
+inputs/outputs, the GELU pre-activation) and recomputes BN/GELU/LN outputs in the
+backward; everything saved goes through ctx.save_for_backward so that
+torch.utils.checkpoint (the reference's per-stage checkpointing,
+tiny_vit.py:170-173) can drop and replay it.  Weight gradients are written by the
+kernels straight into the flat fp32 gradient buffer (optim.FlatParams); the
+Functions return None for every parameter.
+
+Precision policy (mirrors the reference under torch.autocast(bf16),
+SURVEY.md §3.2): bf16 mode = bf16 activations/GEMM operands, fp32 accumulation,
+LayerNorm/BN statistics in fp32, fp32 decoder residual stream with the branch
+rounded to bf16 before the add, bf16 pred, fp32 loss.  fp32 mode = everything
+fp32 (what the reference computes on a CPU-only host) — used for parity.
+"""
+import math
+
+import torch
+
+from . import kernels as K
+
+
+class Mode:
+    __slots__ = ("bf16", "act")
+
+    def __init__(self, bf16):
+        self.bf16 = bool(bf16)
+        self.act = torch.bfloat16 if bf16 else torch.float32
+
+
+def W(p, mode):
+    """GEMM operand view of a weight: bf16 shadow or the fp32 master."""
+    return p._sm_bf16 if mode.bf16 else p.detach()
+
+
+def G(p):
+    return p._sm_grad
+
+
+def _touch(*params):
+    flat = getattr(params[0], "_sm_flat", None)
+    if flat is None:
+        raise RuntimeError("parameters are not registered in a FlatParams buffer")
+    flat.touch(*params)
+
+
+def _bn_forward(a2d, bn, gelu, residual=None, updates=1):
+    mean, rstd = K.bn_stats(a2d, bn.running_mean, bn.running_var, bn.momentum, bn.eps, updates,
+                            bn.num_batches_tracked)
+    y = K.bn_apply(a2d, mean, rstd, bn.weight.detach(), bn.bias.detach(), gelu=gelu, residual=residual)
+    return y, mean, rstd
+
+
+# ============================================================================ stem
+class StemFn(torch.autograd.Function):
+    """PatchEmbed (tiny_vit.py:62-72): conv3x3 s2 3->48, BN, GELU, conv3x3 s1 48->96, BN.
+    Input: the clip [B,3,T,H,W] (or frames [N,3,H,W]); the frame permute of
+    mae_vit_adapter.py:84 is folded into the im2col loads."""
+
+    @staticmethod
+    def forward(ctx, clip, st, w1, g1, b1, w2, g2, b2):
+        mode = st.mode
+        act = mode.act
+        col1, (Fr, Ho, Wo) = K.stem_im2col(clip, act)
+        w1p = K.conv_wpack(w1.detach(), 32, 0, act)
+        a1 = K.linear(col1, w1p)
+        del col1
+        h1, m1, r1 = _bn_forward(a1, st.bn1, gelu=True)
+        col2 = K.im2col3(h1, Fr, Ho, Wo, 48, 1)
+        del h1
+        w2p = K.conv_wpack(w2.detach(), 432, 1, act)
+        a2 = K.linear(col2, w2p)
+        del col2
+        y, m2, r2 = _bn_forward(a2, st.bn2, gelu=False)
+        ctx.st = st
+        ctx.geom = (Fr, Ho, Wo)
+        ctx.params = (w1, g1, b1, w2, g2, b2)
+        ctx.save_for_backward(clip, a1, a2, m1, r1, m2, r2, w1p, w2p)
+        return y.view(Fr, Ho, Wo, 96)
+
+    @staticmethod
+    def backward(ctx, dy):
+        clip, a1, a2, m1, r1, m2, r2, w1p, w2p = ctx.saved_tensors
+        w1, g1, b1, w2, g2, b2 = ctx.params
+        act = ctx.st.mode.act
+        Fr, Ho, Wo = ctx.geom
+        _touch(w1, g1, b1, w2, g2, b2)
+        dy = dy.reshape(-1, 96).to(act).contiguous()
+        da2 = K.bn_bwd(dy, a2, m2, r2, g2.detach(), b2.detach(), False, G(g2), G(b2))
+        del dy
+        h1 = K.bn_apply(a1, m1, r1, g1.detach(), b1.detach(), gelu=True)
+        col2 = K.im2col3(h1, Fr, Ho, Wo, 48, 1)
+        del h1
+        dw2p = torch.empty((96, 432), dtype=torch.float32, device=a1.device)
+        K.linear_dw(da2, col2, dw2p, accumulate=False)
+        del col2
+        K.conv_wunpack_add(dw2p, G(w2), 1)
+        dcol2 = K.linear_dx(da2, w2p)
+        del da2
+        dh1 = K.col2im3(dcol2, Fr, Ho, Wo, 48, 1)
+        del dcol2
+        da1 = K.bn_bwd(dh1, a1, m1, r1, g1.detach(), b1.detach(), True, G(g1), G(b1))
+        del dh1
+        col1, _ = K.stem_im2col(clip, act)
+        dw1p = torch.empty((48, 32), dtype=torch.float32, device=a1.device)
+        K.linear_dw(da1, col1, dw1p, accumulate=False)
+        K.conv_wunpack_add(dw1p, G(w1), 0)
+        return (None,) * 8
+
+
+# ============================================================================ MBConv
+class MBConvFn(torch.autograd.Function):
+    """MBConv + SELayer (tiny_vit.py:36-56, 20-34): 1x1 expand, BN, GELU, dw3x3
+    (stride s), BN, GELU, SE, 1x1 project, BN (+ residual when s == 1, Cin == Cout)."""
+
+    @staticmethod
+    def forward(ctx, x, st, w_exp, g0, b0, w_dw, g2, b2, w_fc0, w_fc2, w_proj, g5, b5):
+        mode = st.mode
+        Fr, H, Wd, Cin = x.shape
+        mid, Cout, s = st.mid, st.cout, st.stride
+        x2d = x.reshape(-1, Cin)
+        a1 = K.linear(x2d, W(w_exp, mode).view(mid, Cin))
+        h1, m0, r0 = _bn_forward(a1, st.bn0, gelu=True)
+        a2 = K.dwconv(h1, w_dw.detach().view(mid, 9), Fr, H, Wd, mid, s)
+        del h1
+        Ho, Wo = (H - 1) // s + 1, (Wd - 1) // s + 1
+        h2, m2, r2 = _bn_forward(a2, st.bn2, gelu=True)
+        h3, pooled, h1se, gate = K.se_fwd(h2, Fr, Ho * Wo, mid, w_fc0.detach(), w_fc2.detach())
+        del h2
+        a3 = K.linear(h3, W(w_proj, mode).view(Cout, mid))
+        del h3
+        out, m5, r5 = _bn_forward(a3, st.bn5, gelu=False, residual=x2d if st.res else None)
+        ctx.st = st
+        ctx.geom = (Fr, H, Wd, Cin, Ho, Wo)
+        ctx.params = (w_exp, g0, b0, w_dw, g2, b2, w_fc0, w_fc2, w_proj, g5, b5)
+        ctx.save_for_backward(x, a1, a2, a3, m0, r0, m2, r2, m5, r5, pooled, h1se, gate)
+        return out.view(Fr, Ho, Wo, Cout)
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, a1, a2, a3, m0, r0, m2, r2, m5, r5, pooled, h1se, gate = ctx.saved_tensors
+        w_exp, g0, b0, w_dw, g2, b2, w_fc0, w_fc2, w_proj, g5, b5 = ctx.params
+        st = ctx.st
+        mode = st.mode
+        Fr, H, Wd, Cin, Ho, Wo = ctx.geom
+        mid, Cout, s = st.mid, st.cout, st.stride
+        _touch(*ctx.params)
+        dout2d = dout.reshape(-1, Cout).to(mode.act).contiguous()
+        da3 = K.bn_bwd(dout2d, a3, m5, r5, g5.detach(), b5.detach(), False, G(g5), G(b5))
+        h2 = K.bn_apply(a2, m2, r2, g2.detach(), b2.detach(), gelu=True)
+        h3 = K.se_scale(h2, gate, Fr, Ho * Wo, mid)
+        K.linear_dw(da3, h3, G(w_proj).view(Cout, mid))
+        del h3
+        dh3 = K.linear_dx(da3, W(w_proj, mode).view(Cout, mid))
+        del da3
+        dh2, dz2, dz1 = K.se_bwd(dh3, h2, Fr, Ho * Wo, mid, w_fc0.detach(), w_fc2.detach(), gate, h1se)
+        del dh3, h2
+        R = mid // 4
+        K.gemm(dz2, h1se, G(w_fc2), mid, R, Fr, 1, 1, mid, R, R, beta=1.0)
+        K.gemm(dz1, pooled, G(w_fc0), R, mid, Fr, 1, 1, R, mid, mid, beta=1.0)
+        da2 = K.bn_bwd(dh2, a2, m2, r2, g2.detach(), b2.detach(), True, G(g2), G(b2))
+        del dh2
+        h1 = K.bn_apply(a1, m0, r0, g0.detach(), b0.detach(), gelu=True)
+        dh1 = K.dwconv_bwd(da2, h1, w_dw.detach().view(mid, 9), G(w_dw).view(mid, 9), Fr, H, Wd, mid, s)
+        del h1, da2
+        da1 = K.bn_bwd(dh1, a1, m0, r0, g0.detach(), b0.detach(), True, G(g0), G(b0))
+        del dh1
+        x2d = x.reshape(-1, Cin)
+        K.linear_dw(da1, x2d, G(w_exp).view(mid, Cin))
+        dx = K.linear_dx(da1, W(w_exp, mode).view(mid, Cin), residual=dout2d if st.res else None)
+        return (dx.view(Fr, H, Wd, Cin),) + (None,) * 12
+
+
+# ============================================================================ transformer block
+class BlockFn(torch.autograd.Function):
+    """Pre-norm transformer block used by both the TinyViT encoder
+    (TinyViTBlock, tiny_vit.py:108-130: global attention, Mlp with GELU) and the MAE
+    decoder (nn.TransformerEncoderLayer(norm_first=True, activation='gelu'),
+    mae_vit_adapter.py:40-48).  x: [N*L, C] residual stream (bf16 in the encoder,
+    fp32 in the decoder)."""
+
+    @staticmethod
+    def forward(ctx, x, st, ln1w, ln1b, wqkv, bqkv, wproj, bproj, ln2w, ln2b, w1, b1, w2, b2):
+        mode = st.mode
+        act = mode.act
+        N, L, H, D = st.N, st.L, st.heads, st.head_dim
+        rb = mode.bf16
+        ln1, mu1, rs1 = K.layernorm(x, ln1w.detach(), ln1b.detach(), out_dtype=act, eps=st.eps)
+        qkv = K.linear(ln1, W(wqkv, mode), bqkv.detach())
+        del ln1
+        o, lse = K.attn_fwd(qkv, N, L, H, D, st.attn_drop, st.seed)
+        x2 = K.linear(o, W(wproj, mode), bproj.detach(), out_dtype=x.dtype, residual=x, round_branch=rb)
+        ln2, mu2, rs2 = K.layernorm(x2, ln2w.detach(), ln2b.detach(), out_dtype=act, eps=st.eps)
+        h, hpre = K.linear(ln2, W(w1, mode), b1.detach(), gelu=True)
+        del ln2
+        out = K.linear(h, W(w2, mode), b2.detach(), out_dtype=x.dtype, residual=x2, round_branch=rb)
+        del h
+        ctx.st = st
+        ctx.params = (ln1w, ln1b, wqkv, bqkv, wproj, bproj, ln2w, ln2b, w1, b1, w2, b2)
+        ctx.save_for_backward(x, mu1, rs1, qkv, o, lse, x2, mu2, rs2, hpre)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, mu1, rs1, qkv, o, lse, x2, mu2, rs2, hpre = ctx.saved_tensors
+        ln1w, ln1b, wqkv, bqkv, wproj, bproj, ln2w, ln2b, w1, b1, w2, b2 = ctx.params
+        st = ctx.st
+        mode = st.mode
+        act = mode.act
+        N, L, H, D = st.N, st.L, st.heads, st.head_dim
+        _touch(*ctx.params)
+        dout = dout.contiguous()
+        if dout.dtype != x.dtype:
+            dout = dout.to(x.dtype)
+        db = dout if dout.dtype == act else K.cast(dout, act)       # grad of the bf16 branch
+        h = K.gelu(hpre)
+        K.linear_dw(db, h, G(w2))
+        K.colsum(db, G(b2))
+        del h
+        dh = K.linear_dx(db, W(w2, mode))
+        del db
+        dhpre = K.gelu_bwd(hpre, dh)
+        del dh
+        ln2 = K.layernorm(x2, ln2w.detach(), ln2b.detach(), out_dtype=act, eps=st.eps)[0]
+        K.linear_dw(dhpre, ln2, G(w1))
+        K.colsum(dhpre, G(b1))
+        del ln2
+        dln2 = K.linear_dx(dhpre, W(w1, mode))
+        del dhpre
+        dx2 = K.layernorm_bwd(dln2, x2, mu2, rs2, ln2w.detach(), G(ln2w), G(ln2b), dres=dout)
+        del dln2
+        dxb = dx2 if dx2.dtype == act else K.cast(dx2, act)
+        K.linear_dw(dxb, o, G(wproj))
+        K.colsum(dxb, G(bproj))
+        do = K.linear_dx(dxb, W(wproj, mode))
+        del dxb
+        dqkv = K.attn_bwd(qkv, o, do, lse, N, L, H, D, st.attn_drop, st.seed)
+        del do
+        ln1 = K.layernorm(x, ln1w.detach(), ln1b.detach(), out_dtype=act, eps=st.eps)[0]
+        K.linear_dw(dqkv, ln1, G(wqkv))
+        K.colsum(dqkv, G(bqkv))
+        del ln1
+        dln1 = K.linear_dx(dqkv, W(wqkv, mode))
+        del dqkv
+        dx = K.layernorm_bwd(dln1, x, mu1, rs1, ln1w.detach(), G(ln1w), G(ln1b), dres=dx2)
+        return (dx,) + (None,) * 13
+
+
+# ============================================================================ enc_to_dec + blend
+class EncToDecFn(torch.autograd.Function):
+    """enc_to_dec Linear + temporal/spatial pos-embed + mask-token blend
+    (mae_vit_adapter.py:90-107).  lat [F*L, 384] -> x [B*T*L, D] fp32."""
+
+    @staticmethod
+    def forward(ctx, lat, mask_u8, st, w, b, tpos, spos, tok):
+        mode = st.mode
+        B, T, L, D = st.B, st.T, st.L, st.D
+        y = K.linear(lat, W(w, mode), b.detach())
+        x = K.pos_blend(y, tpos.detach().reshape(-1, D), spos.detach().reshape(L, D), tok.detach().reshape(D),
+                        mask_u8, B, T, L, D, torch.float32)
+        ctx.st = st
+        ctx.params = (w, b, tpos, spos, tok)
+        ctx.save_for_backward(lat, mask_u8)
+        return x
+
+    @staticmethod
+    def backward(ctx, dx):
+        lat, mask_u8 = ctx.saved_tensors
+        w, b, tpos, spos, tok = ctx.params
+        st = ctx.st
+        mode = st.mode
+        B, T, L, D = st.B, st.T, st.L, st.D
+        _touch(*ctx.params)
+        dx = dx.float().contiguous()
+        dy = K.pos_blend_bwd(dx, mask_u8, mode.act, G(tpos).reshape(-1, D), G(spos).reshape(L, D),
+                             G(tok).reshape(D), B, T, L, D)
+        K.linear_dw(dy, lat, G(w))
+        K.colsum(dy, G(b))
+        dlat = K.linear_dx(dy, W(w, mode))
+        return dlat, None, None, None, None, None, None, None
+
+
+# ============================================================================ head
+class HeadFn(torch.autograd.Function):
+    """decoder_norm + decoder_pred (mae_vit_adapter.py:111-115): x [M, D] -> pred [M, 192]."""
+
+    @staticmethod
+    def forward(ctx, x, st, lnw, lnb, w, b):
+        mode = st.mode
+        ln, mu, rs = K.layernorm(x, lnw.detach(), lnb.detach(), out_dtype=mode.act)
+        pred = K.linear(ln, W(w, mode), b.detach())
+        ctx.st = st
+        ctx.params = (lnw, lnb, w, b)
+        ctx.save_for_backward(x, mu, rs)
+        return pred
+
+    @staticmethod
+    def backward(ctx, dpred):
+        x, mu, rs = ctx.saved_tensors
+        lnw, lnb, w, b = ctx.params
+        mode = ctx.st.mode
+        _touch(*ctx.params)
+        dpred = dpred.to(mode.act).contiguous()
+        ln = K.layernorm(x, lnw.detach(), lnb.detach(), out_dtype=mode.act)[0]
+        K.linear_dw(dpred, ln, G(w))
+        K.colsum(dpred, G(b))
+        del ln
+        dln = K.linear_dx(dpred, W(w, mode))
+        dx = K.layernorm_bwd(dln, x, mu, rs, lnw.detach(), G(lnw), G(lnb))
+        return dx, None, None, None, None, None
+
+
+# ============================================================================ loss
+class MAELossFn(torch.autograd.Function):
+    """patchify + norm_pix (unbiased var) + masked MSE (train_ssl_mae.py:26-31,74-84),
+    fused; the target never exists in HBM."""
+
+    @staticmethod
+    def forward(ctx, pred, clip, mask_u8, norm_pix):
+        clip = clip if clip.dtype == torch.float32 else clip.float()
+        loss, denom = K.mae_loss_fwd(pred.contiguous(), clip, mask_u8, norm_pix)
+        ctx.norm_pix = norm_pix
+        ctx.save_for_backward(pred, clip, mask_u8, denom)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        pred, clip, mask_u8, denom = ctx.saved_tensors
+        dpred = K.mae_loss_bwd(pred.contiguous(), clip, mask_u8, ctx.norm_pix, g, denom)
+        return dpred, None, None, None
+
+
+def mae_loss(pred, clip, mask, norm_pix=True):
+    """Masked normalised-pixel MSE of the reference (train_ssl_mae.py:72-84)."""
+    m = mask if mask.dtype == torch.uint8 else mask.to(torch.uint8)
+    if m.device != pred.device:
+        m = m.to(pred.device)
+    if clip.device != pred.device:
+        clip = clip.to(pred.device)
+    return MAELossFn.apply(pred, clip, m.contiguous(), bool(norm_pix))
+
+
+def masked_pred_std(pred, mask_idx):
+    """pred[mask.bool()].std() (train_ssl_mae.py:105) from the compacted index list."""
+    rows = K.gather_rows(pred.reshape(-1, pred.shape[-1]), mask_idx)
+    return K.std(rows)

@@ -57,11 +57,11 @@ def linear_dx(dy, w, out_dtype=None, residual=None):
     return out
 
 
-def linear_dw(dy, x, grad_sink):
-    """grad_sink[N,K] += dy^T @ x   (fp32 sink)."""
+def linear_dw(dy, x, grad_sink, accumulate=True):
+    """grad_sink[N,K] (+)= dy^T @ x   (fp32 sink; reduction over the M token rows)."""
     M, N = dy.shape
     K = x.shape[1]
-    gemm(dy, x, grad_sink, N, K, M, 1, 1, N, K, K, beta=1.0)
+    gemm(dy, x, grad_sink, N, K, M, 1, 1, N, K, K, beta=1.0 if accumulate else 0.0)
     return grad_sink
 
 
@@ -119,7 +119,7 @@ def layernorm_bwd(dy, x, mean, rstd, gamma, dgamma, dbeta, dres=None):
 
 
 # ------------------------------------------------------------------ BatchNorm (train)
-def bn_stats(x2d, running_mean=None, running_var=None, momentum=0.1, eps=1e-5, updates=1):
+def bn_stats(x2d, running_mean=None, running_var=None, momentum=0.1, eps=1e-5, updates=1, num_batches=None):
     _chk(x2d)
     M, C = x2d.shape
     mean = torch.empty(C, dtype=torch.float32, device=x2d.device)
@@ -127,7 +127,7 @@ def bn_stats(x2d, running_mean=None, running_var=None, momentum=0.1, eps=1e-5, u
     nbytes = query("sm_bn_workspace_bytes", M, C)
     ws = _ws(nbytes, x2d.device)
     call("sm_bn_stats", dt(x2d), M, C, ptr(x2d), ptr(mean), ptr(rstd), ptr(running_mean), ptr(running_var),
-         float(momentum), float(eps), int(updates), ptr(ws), nbytes, stream())
+         ptr(num_batches), float(momentum), float(eps), int(updates), ptr(ws), nbytes, stream())
     return mean, rstd
 
 
@@ -325,6 +325,29 @@ def mae_loss_bwd(pred, clip, mask_u8, norm_pix, grad_out, denom):
     return dpred
 
 
+def patchify(imgs, p=8):
+    _chk(imgs)
+    x = imgs if imgs.dtype == torch.float32 else imgs.float()
+    B, C, T, H, W = x.shape
+    out = torch.empty((B, T * (H // p) * (W // p), p * p * C), dtype=torch.float32, device=x.device)
+    call("sm_patchify", ptr(x), B, C, T, H, W, *x.stride(), p, ptr(out), stream())
+    return out
+
+
+def unpatchify(tokens, C, T, H, W, p=8):
+    _chk(tokens)
+    t = tokens.contiguous().float()
+    B = t.shape[0]
+    out = torch.empty((B, C, T, H, W), dtype=torch.float32, device=t.device)
+    call("sm_unpatchify", ptr(t), B, C, T, H, W, p, ptr(out), stream())
+    return out
+
+
+def scale_(t, a):
+    call("sm_scale", ptr(t), t.numel(), float(a), stream())
+    return t
+
+
 def gather_rows(src2d, idx):
     out = torch.empty((idx.numel(), src2d.shape[1]), dtype=src2d.dtype, device=src2d.device)
     call("sm_gather_rows", dt(src2d), ptr(src2d), ptr(idx), idx.numel(), src2d.shape[1], ptr(out), stream())
@@ -344,6 +367,6 @@ def nonfinite(g, flag):
     call("sm_nonfinite", ptr(g), g.numel(), ptr(flag), stream())
 
 
-def adamw(p, g, m, v, lr, b1, b2, eps, wd, found_inf, step, shadow=None):
+def adamw(p, g, m, v, lr, b1, b2, eps, wd, found_inf, step, shadow=None, advance_step=True):
     call("sm_adamw", ptr(p), ptr(g), ptr(m), ptr(v), ptr(shadow), p.numel(), float(lr), float(b1), float(b2),
-         float(eps), float(wd), ptr(found_inf), ptr(step), stream())
+         float(eps), float(wd), ptr(found_inf), ptr(step), 1 if advance_step else 0, stream())

@@ -1,0 +1,221 @@
+"""TinyViT encoder (reference: src/models/tiny_vit.py), MI355X-native.
+
+Same constructor signatures, module tree and state_dict keys as the reference
+(`tiny_vit_21m_variant`, `TinyViT(img_size, in_chans, embed_dims, depths, num_heads,
+window_sizes, drop_path_rate, use_checkpoint)`, `forward_stage3`), so reference
+checkpoints load unchanged.  The torch sub-modules (nn.Conv2d / nn.BatchNorm2d /
+nn.Linear / nn.LayerNorm) are kept only as parameter/buffer containers with the
+reference's initialisation; compute runs through the fused HIP Functions of
+functions.py on channels-last activations ([frames][H][W][C]), so the reference's
+NCHW<->NLC transposes (tiny_vit.py:122,129) do not exist.
+"""
+import torch
+import torch.nn as nn
+import torch.utils.checkpoint as checkpoint
+
+from .functions import BlockFn, MBConvFn, Mode, StemFn
+
+
+class DropPath(nn.Module):
+    """Stochastic depth placeholder with timm's attribute name (drop_prob)."""
+
+    def __init__(self, drop_prob=0.0):
+        super().__init__()
+        self.drop_prob = drop_prob
+
+
+class _St:
+    """Static per-call configuration handed to a Function (non-tensor)."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+class Conv2d_BN(nn.Sequential):
+    """tiny_vit.py:12-18."""
+
+    def __init__(self, a, b, ks=1, stride=1, pad=0, dilation=1, groups=1, bn_weight_init=1):
+        super().__init__()
+        self.add_module("c", nn.Conv2d(a, b, ks, stride, pad, dilation, groups, bias=False))
+        self.add_module("bn", nn.BatchNorm2d(b))
+        nn.init.constant_(self.bn.weight, bn_weight_init)
+        nn.init.constant_(self.bn.bias, 0)
+
+
+class SELayer(nn.Module):
+    """tiny_vit.py:20-34 (parameters only; fused into MBConvFn)."""
+
+    def __init__(self, channel, reduction=4):
+        super().__init__()
+        self.avg_pool = nn.AdaptiveAvgPool2d(1)
+        self.fc = nn.Sequential(nn.Linear(channel, channel // reduction, bias=False), nn.ReLU(inplace=True),
+                                nn.Linear(channel // reduction, channel, bias=False), nn.Sigmoid())
+
+
+class MBConv(nn.Module):
+    """tiny_vit.py:36-56."""
+
+    def __init__(self, in_chans, out_chans, expand_ratio=4, stride=1, drop_path=0.0):
+        super().__init__()
+        mid = int(in_chans * expand_ratio)
+        if expand_ratio != 4:
+            raise NotImplementedError("only expand_ratio=4 (the reference's only use) is fused")
+        self.in_chans, self.out_chans, self.mid, self.stride = in_chans, out_chans, mid, stride
+        self.use_res_connect = stride == 1 and in_chans == out_chans
+        self.conv = nn.Sequential(
+            Conv2d_BN(in_chans, mid, ks=1), nn.GELU(),
+            Conv2d_BN(mid, mid, ks=3, stride=stride, pad=1, groups=mid), nn.GELU(),
+            SELayer(mid),
+            Conv2d_BN(mid, out_chans, ks=1, bn_weight_init=0))
+        self.drop_path = DropPath(drop_path) if drop_path > 0.0 else nn.Identity()
+
+    def run(self, x, mode):
+        c = self.conv
+        st = _St(mode=mode, mid=self.mid, cout=self.out_chans, stride=self.stride, res=self.use_res_connect,
+                 bn0=c[0].bn, bn2=c[2].bn, bn5=c[5].bn)
+        return MBConvFn.apply(x, st, c[0].c.weight, c[0].bn.weight, c[0].bn.bias, c[2].c.weight, c[2].bn.weight,
+                              c[2].bn.bias, c[4].fc[0].weight, c[4].fc[2].weight, c[5].c.weight, c[5].bn.weight,
+                              c[5].bn.bias)
+
+
+class PatchEmbed(nn.Module):
+    """tiny_vit.py:62-72: conv3x3 s2 -> BN -> GELU -> conv3x3 s1 -> BN."""
+
+    def __init__(self, in_chans, embed_dim):
+        super().__init__()
+        self.patch_embed = nn.Sequential(
+            Conv2d_BN(in_chans, embed_dim // 2, ks=3, stride=2, pad=1), nn.GELU(),
+            Conv2d_BN(embed_dim // 2, embed_dim, ks=3, stride=1, pad=1))
+
+    def run(self, clip, mode):
+        pe = self.patch_embed
+        if pe[0].c.weight.shape[:2] != (48, 3) or pe[2].c.weight.shape[:2] != (96, 48):
+            raise NotImplementedError("fused stem is specialised for 3->48->96 (embed_dims[0]=96)")
+        st = _St(mode=mode, bn1=pe[0].bn, bn2=pe[2].bn)
+        return StemFn.apply(clip, st, pe[0].c.weight, pe[0].bn.weight, pe[0].bn.bias, pe[2].c.weight,
+                            pe[2].bn.weight, pe[2].bn.bias)
+
+
+class Mlp(nn.Module):
+    """tiny_vit.py:74-84."""
+
+    def __init__(self, in_features, hidden_features=None, out_features=None, act_layer=nn.GELU, drop=0.0):
+        super().__init__()
+        out_features = out_features or in_features
+        hidden_features = hidden_features or in_features
+        self.fc1 = nn.Linear(in_features, hidden_features)
+        self.act = act_layer()
+        self.fc2 = nn.Linear(hidden_features, out_features)
+        self.drop = nn.Dropout(drop)
+
+
+class Attention(nn.Module):
+    """tiny_vit.py:86-106 (global softmax attention over all tokens)."""
+
+    def __init__(self, dim, key_dim, num_heads=8, window_size=7):
+        super().__init__()
+        self.num_heads = num_heads
+        self.scale = key_dim ** -0.5
+        self.key_dim = key_dim
+        self.qkv = nn.Linear(dim, key_dim * num_heads * 3)
+        self.proj = nn.Linear(key_dim * num_heads, dim)
+
+
+class TinyViTBlock(nn.Module):
+    """tiny_vit.py:108-130 (window_size accepted and ignored, as in the reference)."""
+
+    def __init__(self, dim, num_heads, window_size=7, mlp_ratio=4.0, drop_path=0.0):
+        super().__init__()
+        self.dim, self.num_heads = dim, num_heads
+        self.norm1 = nn.LayerNorm(dim)
+        self.attn = Attention(dim, key_dim=dim // num_heads, num_heads=num_heads, window_size=window_size)
+        self.drop_path = DropPath(drop_path) if drop_path > 0.0 else nn.Identity()
+        self.norm2 = nn.LayerNorm(dim)
+        self.mlp = Mlp(in_features=dim, hidden_features=int(dim * mlp_ratio))
+
+    def run(self, x, mode):
+        Fr, H, Wd, C = x.shape
+        st = _St(mode=mode, N=Fr, L=H * Wd, heads=self.num_heads, head_dim=C // self.num_heads,
+                 eps=self.norm1.eps, attn_drop=0.0, seed=0)
+        a, m = self.attn, self.mlp
+        y = BlockFn.apply(x.reshape(Fr * H * Wd, C), st, self.norm1.weight, self.norm1.bias, a.qkv.weight,
+                          a.qkv.bias, a.proj.weight, a.proj.bias, self.norm2.weight, self.norm2.bias,
+                          m.fc1.weight, m.fc1.bias, m.fc2.weight, m.fc2.bias)
+        return y.view(Fr, H, Wd, C)
+
+
+class _Stage(nn.Sequential):
+    def run(self, x, mode):
+        for blk in self:
+            x = blk.run(x, mode)
+        return x
+
+
+class TinyViT(nn.Module):
+    """tiny_vit.py:136-186."""
+
+    def __init__(self, img_size=112, in_chans=3, embed_dims=[96, 192, 384, 576], depths=[2, 2, 6, 2],
+                 num_heads=[3, 6, 12, 24], window_sizes=[7, 7, 14, 7], drop_path_rate=0.1, use_checkpoint=True):
+        super().__init__()
+        self.use_checkpoint = use_checkpoint
+        self.embed_dims = list(embed_dims)
+        self.patch_embed = PatchEmbed(in_chans, embed_dims[0])
+        self.stages = nn.ModuleList()
+        dpr = [x.item() for x in torch.linspace(0, drop_path_rate, sum(depths))]
+        cur = 0
+        for i in range(4):
+            blocks = []
+            if i > 0:
+                blocks.append(MBConv(embed_dims[i - 1], embed_dims[i], stride=2))
+            for j in range(depths[i]):
+                if i == 0:
+                    blocks.append(MBConv(embed_dims[i], embed_dims[i], drop_path=dpr[cur]))
+                else:
+                    blocks.append(TinyViTBlock(dim=embed_dims[i], num_heads=num_heads[i],
+                                               window_size=window_sizes[i], drop_path=dpr[cur]))
+                cur += 1
+            self.stages.append(_Stage(*blocks))
+
+    # ------------------------------------------------------------------ internals
+    def _mode(self):
+        return Mode(torch.is_autocast_enabled("cuda"))
+
+    def _run_stages(self, x, n_stages, mode):
+        for i in range(n_stages):
+            stage = self.stages[i]
+            if self.use_checkpoint and self.training:
+                x = checkpoint.checkpoint(stage.run, x, mode, use_reentrant=False)
+            else:
+                x = stage.run(x, mode)
+        return x
+
+    def tokens_stage3(self, clip, mode):
+        """clip [B,3,T,H,W] or frames [N,3,H,W] -> channels-last [N*T, H/8, W/8, 384]."""
+        x = self.patch_embed.run(clip, mode)
+        return self._run_stages(x, 3, mode)
+
+    def _prepare(self, mode):
+        from .mae_vit_adapter import ensure_flat
+        ensure_flat(self, mode)
+
+    # ------------------------------------------------------------------ reference API
+    def forward_stage3(self, x):
+        """MAE entry point (tiny_vit.py:166-176): [N,3,H,W] -> [N,384,H/8,W/8] (NCHW view)."""
+        mode = self._mode()
+        self._prepare(mode)
+        t = self.tokens_stage3(x, mode)
+        return t.permute(0, 3, 1, 2)
+
+    def forward(self, x):
+        """All four stages (tiny_vit.py:178-186) -> [N, C4, H/16, W/16] (NCHW view)."""
+        mode = self._mode()
+        self._prepare(mode)
+        t = self.patch_embed.run(x, mode)
+        t = self._run_stages(t, 4, mode)
+        return t.permute(0, 3, 1, 2)
+
+
+def tiny_vit_21m_variant(img_size=112, use_checkpoint=True, **kwargs):
+    """tiny_vit.py:188-191."""
+    return TinyViT(img_size=img_size, embed_dims=[96, 192, 384, 576], depths=[2, 2, 6, 2],
+                   num_heads=[3, 6, 12, 18], use_checkpoint=use_checkpoint, **kwargs)

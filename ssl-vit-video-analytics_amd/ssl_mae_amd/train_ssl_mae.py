@@ -1,0 +1,138 @@
+"""MAE pretraining driver (reference: src/train_ssl_mae.py), MI355X-native.
+
+`patchify(imgs, p)` and `train_one_epoch(model, loader, optimizer, scaler, epoch,
+device, config, writer, logger)` keep the reference's signatures and per-step
+semantics (train_ssl_mae.py:52-123): tube mask -> forward under bf16 autocast ->
+masked normalised-pixel MSE -> zero_grad / backward / step -> `loss.item()` every
+step, and every `log_interval` steps the masked-prediction std and throughput
+(log_interval * batch_size / elapsed).  `main()` honours `--config` (the
+reference hard-codes the path, :130) and runs the loop the reference's :168
+TypeError prevents.
+"""
+import argparse
+import logging
+import time
+from datetime import timedelta
+from pathlib import Path
+
+import torch
+
+from . import kernels as K
+from .functions import mae_loss, masked_pred_std
+from .mae_loader import tube_mask_with_index
+from .mae_vit_adapter import TinyVideoMAE
+from .optim import FusedAdamW, GradScaler
+from .tiny_vit import tiny_vit_21m_variant
+from .utils import load_config, save_checkpoint, set_seed
+
+
+def format_time(seconds):
+    return str(timedelta(seconds=int(seconds)))
+
+
+def patchify(imgs, p=8):
+    """[B,C,T,H,W] -> [B, T*(H/p)*(W/p), p*p*C]; token (t,h,w), feature (pi,qi,c)."""
+    return K.patchify(imgs, p)
+
+
+def unpatchify(tokens, C, T, H, W, p=8):
+    """Exact inverse of patchify (the reference's visualize_mae.py:30 einsum drops q)."""
+    return K.unpatchify(tokens, C, T, H, W, p)
+
+
+def setup_logger(save_dir):
+    log_dir = Path("logs") / Path(save_dir).name
+    log_dir.mkdir(parents=True, exist_ok=True)
+    logging.basicConfig(level=logging.INFO, format="%(asctime)s - %(levelname)s - %(message)s",
+                        handlers=[logging.FileHandler(log_dir / "train.log"), logging.StreamHandler()])
+    return logging.getLogger(__name__), log_dir
+
+
+class NullWriter:
+    def add_scalar(self, *a, **k):
+        pass
+
+
+def train_step(model, clip, optimizer, scaler, ssl_cfg, bf16=True):
+    """One iteration of train_one_epoch's body; returns (loss tensor, pred, mask index)."""
+    B, C, T, H, W = clip.shape
+    L = (H // 8) * (W // 8)
+    mask, idx = tube_mask_with_index(B, T, L, ssl_cfg["mask_ratio"], device=clip.device)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=bf16):
+        pred = model(clip, mask)
+    loss = mae_loss(pred, clip, mask, ssl_cfg.get("norm_pix_loss", True))
+    optimizer.zero_grad()
+    scaler.scale(loss).backward()
+    scaler.step(optimizer)
+    scaler.update()
+    return loss, pred, idx
+
+
+def train_one_epoch(model, loader, optimizer, scaler, epoch, device, config, writer, logger):
+    model.train()
+    ssl_cfg = config["ssl"]
+    train_cfg = config["training"]
+    num_steps = len(loader)
+    batch_size = train_cfg["batch_size"]
+    epoch_start = time.time()
+    last_log = time.time()
+    total_loss = 0.0
+    for step, clip in enumerate(loader):
+        clip = clip.to(device, non_blocking=True)
+        loss, pred, idx = train_step(model, clip, optimizer, scaler, ssl_cfg)
+        total_loss += loss.item()
+        if step % train_cfg["log_interval"] == 0 and step > 0:
+            now = time.time()
+            throughput = (train_cfg["log_interval"] * batch_size) / (now - last_log)
+            eta = (now - epoch_start) / (step + 1) * (num_steps - step - 1)
+            pred_std = masked_pred_std(pred, idx).item()
+            logger.info(f"Epoch [{epoch}] [{step:4d}/{num_steps}] Loss: {loss.item():.4f} | Std: {pred_std:.3f} | "
+                        f"Speed: {throughput:.1f} samples/s | Epoch ETA: {format_time(eta)}")
+            last_log = now
+            gstep = (epoch - 1) * num_steps + step
+            writer.add_scalar("Train/Loss", loss.item(), gstep)
+            writer.add_scalar("Train/Throughput", throughput, gstep)
+    return total_loss / max(num_steps, 1), time.time() - epoch_start
+
+
+def build_model(cfg, device="cuda"):
+    encoder = tiny_vit_21m_variant(img_size=cfg["dataset"]["image_size"], use_checkpoint=True)
+    return TinyVideoMAE(encoder, cfg).to(device)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="configs/ssl_mae.yaml")
+    args = ap.parse_args(argv)
+    cfg = load_config(args.config)
+    set_seed(42)
+    device = torch.device("cuda")
+    logger, log_dir = setup_logger(cfg["training"]["save_dir"])
+    try:
+        from torch.utils.tensorboard import SummaryWriter
+        writer = SummaryWriter(log_dir=str(log_dir / "tensorboard"))
+    except Exception:
+        writer = NullWriter()
+    model = build_model(cfg, device)
+    from .data import LazyVideoMAEDataset, make_loader
+    ds = LazyVideoMAEDataset(split_file=cfg["dataset"]["train_split"], clip_len=cfg["dataset"]["clip_len"],
+                             stride=cfg["dataset"]["stride"], image_size=cfg["dataset"]["image_size"])
+    loader = make_loader(ds, cfg["training"]["batch_size"], cfg["training"].get("num_workers", 8))
+    optimizer = FusedAdamW(model.parameters(), lr=float(cfg["training"]["lr"]),
+                           weight_decay=float(cfg["training"].get("weight_decay", 0.05)))
+    scaler = GradScaler("cuda")
+    logger.info(f"STARTING PRETRAINING | epochs {cfg['training']['epochs']} | image {cfg['dataset']['image_size']} | "
+                f"mask ratio {cfg['ssl']['mask_ratio']} | clip_len {cfg['dataset']['clip_len']}")
+    t0 = time.time()
+    for epoch in range(1, cfg["training"]["epochs"] + 1):
+        avg, dur = train_one_epoch(model, loader, optimizer, scaler, epoch, device, cfg, writer, logger)
+        logger.info(f"==> Epoch {epoch} | Average Loss: {avg:.4f} | Time: {format_time(dur)} | "
+                    f"Cumulative: {format_time(time.time() - t0)}")
+        if epoch % 10 == 0:
+            p = Path(cfg["training"]["save_dir"]) / f"encoder_ep{epoch}.pth"
+            save_checkpoint(model.encoder.state_dict(), p)
+            logger.info(f"Checkpoint saved to {p}")
+
+
+if __name__ == "__main__":
+    main()
