@@ -1,0 +1,228 @@
+"""Benchmark: clips/s of the MAE pretraining step (BASELINE.json config 2:
+ViT-Tiny (TinyViT-21M variant) MAE, bf16, batch 256 per GPU, 8x3x224x224
+synthetic clips, mask ratio 0.75) on N GPUs of one node.
+
+One step = tube mask + forward (bf16 autocast) + fused masked-recon loss +
+backward + data-parallel gradient all-reduce (N > 1) + AdamW, exactly the body of
+train_one_epoch (train_ssl_mae.py:66-91) with inputs already resident in HBM.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+Rank 0 prints one JSON line (see the driver contract in DESIGN.md).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "ssl-vit-video-analytics_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "clips/sec (8x3x224x224) MAE ViT-Tiny pretrain, 1/2/4/8 GPU + recon-loss parity"
+FWD_GFLOP_PER_CLIP = 739.0            # SURVEY.md §8(d), T=8, 224^2 (MATH-SDPA FlopCounter)
+TRAIN_TFLOP_PER_CLIP = 3 * FWD_GFLOP_PER_CLIP / 1000.0
+MFMA_BF16_PEAK_TFLOPS = 2500.0        # MI355X dense bf16 (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=256, help="clips per GPU")
+    ap.add_argument("--frames", type=int, default=8)
+    ap.add_argument("--size", type=int, default=224)
+    ap.add_argument("--mask-ratio", type=float, default=0.75)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--probe", default="dec_attn_fwd",
+                    help="kernel group timed with events for the roofline line")
+    return ap.parse_args()
+
+
+def cpu_baseline(T, S, ratio):
+    """The CPU oracle (fp32 restatement of the reference path) timed on the host
+    cores: ONE clip, one fwd+bwd+AdamW step (bounded sample, ~10-30 s)."""
+    from oracle import mae_oracle as O
+    from ssl_mae_amd.init_rule import param_value, synthetic_clip
+    cfg = {"dataset": {"clip_len": T, "image_size": S},
+           "model": {"decoder_embed_dim": 384, "decoder_depth": 4, "decoder_num_heads": 6},
+           "ssl": {"mask_ratio": ratio, "norm_pix_loss": True}}
+    threads = torch.get_num_threads()
+    P = O.make_params(cfg, param_value)
+    bufs = O.init_buffers(P)
+    opt = O.AdamWState(lr=5e-4)
+    clip = torch.from_numpy(synthetic_clip(1, T, S, seed=7))
+    torch.manual_seed(42)
+    mask = O.get_tube_mask(1, T, (S // 8) ** 2, ratio)
+    t0 = time.perf_counter()
+    O.train_step(P, bufs, opt, clip, mask, cfg)
+    dt = time.perf_counter() - t0
+    return {"value": round(1.0 / dt, 5), "unit": "clips/s", "cores": threads, "kind": "port",
+            "sample": f"1 clip {T}x3x{S}x{S}, one fp32 fwd+bwd+AdamW step of oracle/mae_oracle.py "
+                      f"(dropout off) on {threads} host threads; {dt:.1f} s"}
+
+
+class Probe:
+    """HIP-event timing of one kernel group on the stream it is launched on."""
+
+    def __init__(self, name):
+        self.name = name
+        self.pairs = []
+        self.active = False
+
+    def wrap(self, mod, fn_name, select):
+        orig = getattr(mod, fn_name)
+        probe = self
+
+        def wrapped(*a, **k):
+            if probe.active and select(*a, **k):
+                s = torch.cuda.Event(enable_timing=True)
+                e = torch.cuda.Event(enable_timing=True)
+                s.record()
+                out = orig(*a, **k)
+                e.record()
+                probe.pairs.append((s, e))
+                return out
+            return orig(*a, **k)
+        setattr(mod, fn_name, wrapped)
+
+    def avg_ms(self):
+        if not self.pairs:
+            return None
+        return sum(s.elapsed_time(e) for s, e in self.pairs) / len(self.pairs)
+
+
+def main():
+    args = parse()
+    from ssl_mae_amd import dist as smdist
+    from ssl_mae_amd import kernels as K
+    from ssl_mae_amd.build import build
+    rank, world = smdist.init_from_env()
+    if world == 1 and args.gpus > 1 and rank == 0:
+        print(f"[bench] --gpus {args.gpus} without torchrun: running one process", file=sys.stderr)
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if rank == 0:
+        build()
+    if world > 1:
+        dist.barrier()
+
+    from ssl_mae_amd.init_rule import IMAGENET_MEAN, IMAGENET_STD
+    from ssl_mae_amd.optim import FusedAdamW, GradScaler
+    from ssl_mae_amd.train_ssl_mae import build_model, train_step
+
+    B, T, S, r = args.batch, args.frames, args.size, args.mask_ratio
+    cfg = {"dataset": {"clip_len": T, "image_size": S, "stride": 4, "train_split": "-"},
+           "model": {"decoder_embed_dim": 384, "decoder_depth": 4, "decoder_num_heads": 6},
+           "ssl": {"mask_ratio": r, "norm_pix_loss": True},
+           "training": {"batch_size": B, "lr": 5e-4, "log_interval": 20}}
+    torch.manual_seed(1234)                      # identical initial weights on every replica
+    model = build_model(cfg, dev).train()
+    torch.manual_seed(4321 + rank)               # per-rank mask stream
+    opt = FusedAdamW(model.parameters(), lr=5e-4, weight_decay=0.05)
+    scaler = GradScaler()
+    # synthetic clips resident in HBM: (U[0,1) - mean_c) / std_c, per rank
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    mean = torch.tensor(IMAGENET_MEAN, device=dev).view(1, 3, 1, 1, 1)
+    std = torch.tensor(IMAGENET_STD, device=dev).view(1, 3, 1, 1, 1)
+    clips = [((torch.rand(B, 3, T, S, S, generator=g, device=dev) - mean) / std) for _ in range(2)]
+
+    probe = Probe(args.probe)
+    Ld = T * (S // 8) ** 2
+    if args.probe == "dec_attn_fwd":
+        probe.wrap(K, "attn_fwd", lambda qkv, N, L, H, D, *a, **k: D == 64 and L == Ld)
+        flop_per_launch = 4.0 * B * 6 * Ld * Ld * 64
+    elif args.probe == "dec_attn_bwd":
+        probe.wrap(K, "attn_bwd", lambda qkv, o, do, lse, N, L, H, D, *a, **k: D == 64 and L == Ld)
+        flop_per_launch = 14.0 * B * 6 * Ld * Ld * 64   # dK/dV pass (4 products) + dQ pass (3)
+    else:
+        flop_per_launch = None
+
+    ssl_cfg = cfg["ssl"]
+    if world > 1:
+        opt.grad_hooks.append(smdist.GradAllReduce(world))
+
+    def step(i):
+        loss, _, _ = train_step(model, clips[i % 2], opt, scaler, ssl_cfg, bf16=True)
+        return loss
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    probe.active = True
+    t0 = time.perf_counter()
+    losses = []
+    for i in range(args.steps):
+        losses.append(step(i))
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    probe.active = False
+    if world > 1:
+        dist.barrier()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    loss_vals = [float(l.item()) for l in losses]
+    peak_mem = torch.cuda.max_memory_allocated(dev) / 2 ** 30
+
+    if rank == 0:
+        clips_total = B * world * args.steps
+        value = clips_total / elapsed
+        ms = elapsed / args.steps * 1e3
+        roof = None
+        avg = probe.avg_ms()
+        if avg and flop_per_launch:
+            achieved = flop_per_launch / (avg * 1e-3) / 1e12
+            roof = {"kernel": args.probe, "bound": "mfma", "achieved": round(achieved, 1),
+                    "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None,
+                    "avg_launch_ms": round(avg, 3), "launches": len(probe.pairs),
+                    "algorithmic_flop_per_launch": flop_per_launch}
+        step_tflops = value / world * TRAIN_TFLOP_PER_CLIP
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            try:
+                cpu = cpu_baseline(T, S, r)
+            except Exception as e:  # the baseline must not kill the bench line
+                cpu = {"value": None, "error": repr(e)[:200]}
+        line = {
+            "metric": METRIC, "value": round(value, 3), "unit": "clips/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 2),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (U[0,1) ImageNet-normalised clips in HBM; random-init weights)",
+            "config": {"workload": "BASELINE config 2: TinyViT-21M-variant MAE (stem+stages 1-3) + 4x384 decoder, "
+                                   "T=8, 224x224, mask 0.75, bf16 autocast",
+                       "model": "tiny_vit_21m_variant + TinyVideoMAE", "global_batch": B * world,
+                       "per_gpu_batch": B, "frames": T, "image_size": S, "mask_ratio": r,
+                       "parallelism": f"dp{world}"},
+            "roofline": roof,
+            "model_tflops_per_gpu": round(step_tflops, 1),
+            "model_mfu": round(step_tflops / MFMA_BF16_PEAK_TFLOPS, 4),
+            "peak_mem_gib": round(peak_mem, 1),
+            "loss_first_last": [round(loss_vals[0], 5), round(loss_vals[-1], 5)],
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -111,5 +111,40 @@ SM_DEV float uniform01(uint64_t seed, uint64_t idx) {
   return (mix32(seed, idx) >> 8) * (1.0f / 16777216.0f);
 }
 
+// Reduce partial slabs part[nb][ncols] over nb.  Block = 32 columns x 8 row groups;
+// fp64 accumulation, fixed order (deterministic).  Writes fp64 (outd) and/or
+// fp32 (outf, optionally accumulating).
+static __global__ __launch_bounds__(256) void colred_kernel(const float* part, int nb, int ncols, double* outd,
+                                                     float* outf, int accumulate) {
+  __shared__ double red[8][32];
+  const int cl = threadIdx.x & 31, g = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  if (c < ncols) {
+    int b = g;
+    for (; b + 24 < nb; b += 32) {
+      s0 += part[(int64_t)b * ncols + c];
+      s1 += part[(int64_t)(b + 8) * ncols + c];
+      s2 += part[(int64_t)(b + 16) * ncols + c];
+      s3 += part[(int64_t)(b + 24) * ncols + c];
+    }
+    for (; b < nb; b += 8) s0 += part[(int64_t)b * ncols + c];
+  }
+  red[g][cl] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (g == 0 && c < ncols) {
+    double t = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += red[k][cl];
+    if (outd) outd[c] = t;
+    if (outf) outf[c] = accumulate ? outf[c] + (float)t : (float)t;
+  }
+}
+
+static inline void colred(const float* part, int nb, int ncols, double* outd, float* outf, int accumulate, hipStream_t st) {
+  hipLaunchKernelGGL(colred_kernel, dim3((ncols + 31) / 32), dim3(256), 0, st, part, nb, ncols, outd, outf,
+                     accumulate);
+}
+
 #define SM_CHECK_LAUNCH() \
   do { hipError_t e__ = hipGetLastError(); if (e__ != hipSuccess) return (int)e__; } while (0)

@@ -137,14 +137,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* dy, const TI* x, 
   }
 }
 
-// out[c] (+)= sum_b part[b][c]   (fp64 accumulation; one thread per column)
-__global__ void colsum_kernel(const float* part, int nb, int C, float* out, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0;
-  for (int b = 0; b < nb; ++b) s += part[(int64_t)b * C + c];
-  out[c] = accumulate ? out[c] + (float)s : (float)s;
-}
+
 
 // ============================================================ BatchNorm (train)
 // Thread layout shared by the column-reduction kernels: thread t owns the 4-wide
@@ -196,17 +189,13 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const T* x, int64_t M, in
 }
 
 template <typename T>
-__global__ void bn_finalize_kernel(const float* part, int nb, const T* x, int64_t M, int C, float eps,
+__global__ void bn_finalize_kernel(const double* sums /*[2][C]*/, const T* x, int64_t M, int C, float eps,
                                    float momentum, float* mean_out, float* rstd_out, float* run_mean,
                                    float* run_var, int updates, int64_t* nbt) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c == 0 && nbt) *nbt += updates;
   if (c >= C) return;
-  double s = 0.0, q = 0.0;
-  for (int b = 0; b < nb; ++b) {
-    s += part[((int64_t)b * 2 + 0) * C + c];
-    q += part[((int64_t)b * 2 + 1) * C + c];
-  }
+  const double s = sums[c], q = sums[C + c];
   const double shift = (double)to_f<T>(x[c]);
   const double md = s / (double)M;
   double var = q / (double)M - md * md;
@@ -226,27 +215,50 @@ __global__ void bn_finalize_kernel(const float* part, int nb, const T* x, int64_
   }
 }
 
+// Channel-owning layout for [M][C] streaming kernels: thread t owns the 8-channel
+// chunk t % (C/8) for rows t / (C/8) (+ k * rows-per-pass); per-channel parameters
+// live in registers and rows are walked with 16-byte loads.
+struct Col8 {
+  int nch, rpp, chunk, r;
+  SM_DEV Col8(int C) {
+    nch = C / 8;
+    rpp = 256 / nch;
+    if (rpp < 1) rpp = 1;
+    chunk = threadIdx.x % nch;
+    r = threadIdx.x / nch;
+  }
+  SM_DEV bool active() const { return r < rpp; }
+};
+
 template <typename TI, typename TO>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const TI* x, const float* mean, const float* rstd,
-                                                       const float* w, const float* b, TO* y,
-                                                       int64_t total8, int C, int gelu, const TO* R) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total8;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t e = i * 8;
-    const int c0 = (int)(e % C);
+                                                       const float* w, const float* b, TO* y, int64_t M, int C,
+                                                       int rows_per_block, int gelu, const TO* R) {
+  Col8 cm(C);
+  if (!cm.active()) return;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = cm.chunk * 8 + j;
+    sc[j] = rstd[c] * w[c];
+    sh[j] = b[c] - mean[c] * sc[j];
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
+  for (int64_t row = r0 + cm.r; row < r1; row += cm.rpp) {
+    const int64_t e = row * C + cm.chunk * 8;
     float v[8];
     load8(x + e, v);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int c = c0 + j;
-      float t = (v[j] - mean[c]) * rstd[c] * w[c] + b[c];
+      const float t = v[j] * sc[j] + sh[j];
       v[j] = gelu ? gelu_f(t) : t;
     }
     if (R) {
-      float r[8];
-      load8(R + e, r);
+      float rr[8];
+      load8(R + e, rr);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] += r[j];
+      for (int j = 0; j < 8; ++j) v[j] += rr[j];
     }
     store8(y + e, v);
   }
@@ -301,15 +313,11 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const TD* dy, const 
 }
 
 // sums -> dgamma (+=), dbeta (+=), and the two per-channel coefficients for dx
-__global__ void bn_bwd_finalize_kernel(const float* part, int nb, int64_t M, int C, float* dw, float* db,
+__global__ void bn_bwd_finalize_kernel(const double* sums /*[2][C]*/, int64_t M, int C, float* dw, float* db,
                                        float* coef /*[2][C]: mean(g), mean(g*xhat)*/) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  double a = 0.0, b = 0.0;
-  for (int k = 0; k < nb; ++k) {
-    a += part[((int64_t)k * 2 + 0) * C + c];
-    b += part[((int64_t)k * 2 + 1) * C + c];
-  }
+  const double a = sums[c], b = sums[C + c];
   if (dw) dw[c] += (float)b;
   if (db) db[c] += (float)a;
   coef[c] = (float)(a / (double)M);
@@ -319,22 +327,30 @@ __global__ void bn_bwd_finalize_kernel(const float* part, int nb, int64_t M, int
 template <typename TI, typename TD, typename TX>
 __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const TD* dy, const TI* x, const float* mean,
                                                         const float* rstd, const float* w, const float* b,
-                                                        const float* coef, TX* dx, int64_t total8, int C,
-                                                        int gelu) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total8;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t e = i * 8;
-    const int c0 = (int)(e % C);
+                                                        const float* coef, TX* dx, int64_t M, int C,
+                                                        int rows_per_block, int gelu) {
+  Col8 cm(C);
+  if (!cm.active()) return;
+  float mu[8], rs[8], ww[8], bb[8], k0[8], k1[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = cm.chunk * 8 + j;
+    mu[j] = mean[c]; rs[j] = rstd[c]; ww[j] = w[c]; bb[j] = b[c];
+    k0[j] = coef[c]; k1[j] = coef[C + c];
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
+  for (int64_t row = r0 + cm.r; row < r1; row += cm.rpp) {
+    const int64_t e = row * C + cm.chunk * 8;
     float xv[8], dv[8], o[8];
     load8(x + e, xv);
     load8(dy + e, dv);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int c = c0 + j;
-      const float xh = (xv[j] - mean[c]) * rstd[c];
+      const float xh = (xv[j] - mu[j]) * rs[j];
       float gg = dv[j];
-      if (gelu) gg *= gelu_grad(xh * w[c] + b[c]);
-      o[j] = w[c] * rstd[c] * (gg - coef[c] - xh * coef[C + c]);
+      if (gelu) gg *= gelu_grad(xh * ww[j] + bb[j]);
+      o[j] = ww[j] * rs[j] * (gg - k0[j] - xh * k1[j]);
     }
     store8(dx + e, o);
   }
@@ -421,6 +437,12 @@ inline int ew_blocks(int64_t n8) {
   if (b > 8192) b = 8192;
   return b < 1 ? 1 : (int)b;
 }
+// rows per block for the channel-owning streaming kernels (~4096 blocks)
+inline int stream_rows_per_block(int64_t M) {
+  int64_t r = (M + 4095) / 4096;
+  if (r < 16) r = 16;
+  return (int)r;
+}
 inline int red_rows_per_block(int64_t M, int C) {
   // aim for ~2048 blocks, at least 64 rows each
   int64_t r = (M + 2047) / 2048;
@@ -452,7 +474,7 @@ extern "C" int sm_layernorm_fwd(int x_dtype, int y_dtype, int64_t M, int C, cons
 }
 
 extern "C" int64_t sm_layernorm_bwd_workspace_bytes(int64_t M, int C) {
-  const int64_t rpb = 64;
+  const int64_t rpb = red_rows_per_block(M, C);
   const int64_t nb = (M + rpb - 1) / rpb;
   return nb * C * 4 * 2;
 }
@@ -464,7 +486,7 @@ extern "C" int sm_layernorm_bwd(int x_dtype, int dy_dtype, int dx_dtype, int64_t
                                 int64_t ws_bytes, hipStream_t st) {
   if (M <= 0) return 0;
   if (C % 4 || C > 1024) return -2;
-  const int rpb = 64;
+  const int rpb = red_rows_per_block(M, C);
   const int nb = (int)((M + rpb - 1) / rpb);
   if (ws_bytes < (int64_t)nb * C * 8) return -4;
   float* pg = (float*)ws;
@@ -474,8 +496,8 @@ extern "C" int sm_layernorm_bwd(int x_dtype, int dy_dtype, int dx_dtype, int64_t
             hipLaunchKernelGGL((ln_bwd_kernel<T1, T2, T1>), dim3(nb), dim3(256), 0, st, (const T2*)dy,
                                (const T1*)x, mean, rstd, gamma, (T1*)dx, pg, pb, M, C, rpb, (const T1*)dres));
   SM_CHECK_LAUNCH();
-  hipLaunchKernelGGL(colsum_kernel, dim3((C + 255) / 256), dim3(256), 0, st, pg, nb, C, dgamma, 1);
-  hipLaunchKernelGGL(colsum_kernel, dim3((C + 255) / 256), dim3(256), 0, st, pb, nb, C, dbeta, 1);
+  colred(pg, nb, C, nullptr, dgamma, 1, st);
+  colred(pb, nb, C, nullptr, dbeta, 1, st);
   SM_CHECK_LAUNCH();
   return 0;
 }
@@ -483,7 +505,7 @@ extern "C" int sm_layernorm_bwd(int x_dtype, int dy_dtype, int dx_dtype, int64_t
 extern "C" int64_t sm_bn_workspace_bytes(int64_t M, int C) {
   const int64_t rpb = red_rows_per_block(M, C);
   const int64_t nb = (M + rpb - 1) / rpb;
-  return nb * 2 * C * 4 + 2 * C * 4;
+  return nb * 2 * C * 4 + 2 * C * 8 + 2 * C * 4 + 64;
 }
 
 // batch statistics -> mean/rstd (+ running-stat update `updates` times)
@@ -494,16 +516,19 @@ extern "C" int sm_bn_stats(int x_dtype, int64_t M, int C, const void* x, float* 
   if (C % 4 || C / 4 > 256) return -2;
   const int rpb = red_rows_per_block(M, C);
   const int nb = (int)((M + rpb - 1) / rpb);
-  if (ws_bytes < (int64_t)nb * 2 * C * 4) return -4;
+  if (ws_bytes < (int64_t)nb * 2 * C * 4 + 2 * C * 8 + 8) return -4;
   float* part = (float*)ws;
+  double* sums = (double*)(((uintptr_t)(part + (int64_t)nb * 2 * C) + 7) & ~(uintptr_t)7);
   if (x_dtype == SM_BF16) {
     hipLaunchKernelGGL(bn_stats_kernel<__bf16>, dim3(nb), dim3(256), 0, st, (const __bf16*)x, M, C, rpb, part);
-    hipLaunchKernelGGL(bn_finalize_kernel<__bf16>, dim3((C + 127) / 128), dim3(128), 0, st, part, nb,
+    colred(part, nb, 2 * C, sums, nullptr, 0, st);
+    hipLaunchKernelGGL(bn_finalize_kernel<__bf16>, dim3((C + 127) / 128), dim3(128), 0, st, sums,
                        (const __bf16*)x, M, C, eps, momentum, mean, rstd, run_mean, run_var, updates,
                        num_batches_tracked);
   } else {
     hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(nb), dim3(256), 0, st, (const float*)x, M, C, rpb, part);
-    hipLaunchKernelGGL(bn_finalize_kernel<float>, dim3((C + 127) / 128), dim3(128), 0, st, part, nb,
+    colred(part, nb, 2 * C, sums, nullptr, 0, st);
+    hipLaunchKernelGGL(bn_finalize_kernel<float>, dim3((C + 127) / 128), dim3(128), 0, st, sums,
                        (const float*)x, M, C, eps, momentum, mean, rstd, run_mean, run_var, updates,
                        num_batches_tracked);
   }
@@ -515,11 +540,12 @@ extern "C" int sm_bn_apply(int x_dtype, int y_dtype, int64_t M, int C, const voi
                            const float* rstd, const float* w, const float* b, void* y, int gelu,
                            const void* R, hipStream_t st) {
   if (M <= 0) return 0;
-  if (C % 8) return -2;
-  const int64_t n8 = M * C / 8;
+  if (C % 8 || C / 8 > 256) return -2;
+  const int rpb = stream_rows_per_block(M);
+  const int nb = (int)((M + rpb - 1) / rpb);
   DISPATCH2(x_dtype, y_dtype,
-            hipLaunchKernelGGL((bn_apply_kernel<T1, T2>), dim3(ew_blocks(n8)), dim3(256), 0, st, (const T1*)x,
-                               mean, rstd, w, b, (T2*)y, n8, C, gelu, (const T2*)R));
+            hipLaunchKernelGGL((bn_apply_kernel<T1, T2>), dim3(nb), dim3(256), 0, st, (const T1*)x,
+                               mean, rstd, w, b, (T2*)y, M, C, rpb, gelu, (const T2*)R));
   SM_CHECK_LAUNCH();
   return 0;
 }
@@ -531,17 +557,20 @@ extern "C" int sm_bn_bwd(int x_dtype, int g_dtype, int64_t M, int C, const void*
   if (C % 8 || C / 4 > 256) return -2;
   const int rpb = red_rows_per_block(M, C);
   const int nb = (int)((M + rpb - 1) / rpb);
-  if (ws_bytes < (int64_t)nb * 2 * C * 4 + 2 * C * 4) return -4;
+  if (ws_bytes < (int64_t)nb * 2 * C * 4 + 2 * C * 8 + 2 * C * 4 + 8) return -4;
   float* part = (float*)ws;
-  float* coef = part + (int64_t)nb * 2 * C;
+  double* sums = (double*)(((uintptr_t)(part + (int64_t)nb * 2 * C) + 7) & ~(uintptr_t)7);
+  float* coef = (float*)(sums + 2 * C);
   DISPATCH2(x_dtype, g_dtype,
             hipLaunchKernelGGL((bn_bwd_reduce_kernel<T1, T2>), dim3(nb), dim3(256), 0, st, (const T2*)dy,
                                (const T1*)x, mean, rstd, w, b, M, C, rpb, gelu, part));
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 127) / 128), dim3(128), 0, st, part, nb, M, C, dw, db, coef);
-  const int64_t n8 = M * C / 8;
+  colred(part, nb, 2 * C, sums, nullptr, 0, st);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 127) / 128), dim3(128), 0, st, sums, M, C, dw, db, coef);
+  const int srpb = stream_rows_per_block(M);
+  const int snb = (int)((M + srpb - 1) / srpb);
   DISPATCH2(x_dtype, g_dtype,
-            hipLaunchKernelGGL((bn_bwd_dx_kernel<T1, T2, T2>), dim3(ew_blocks(n8)), dim3(256), 0, st,
-                               (const T2*)dy, (const T1*)x, mean, rstd, w, b, coef, (T2*)dx, n8, C, gelu));
+            hipLaunchKernelGGL((bn_bwd_dx_kernel<T1, T2, T2>), dim3(snb), dim3(256), 0, st,
+                               (const T2*)dy, (const T1*)x, mean, rstd, w, b, coef, (T2*)dx, M, C, srpb, gelu));
   SM_CHECK_LAUNCH();
   return 0;
 }
@@ -602,8 +631,7 @@ extern "C" int sm_colsum(int dtype, int64_t M, int C, const void* x, float* out,
     else
       hipLaunchKernelGGL(colsum_part_kernel<float>, dim3(nb), dim3(256), 0, st, (const float*)xs, (int64_t)C, M, cs,
                          rpb, part);
-    hipLaunchKernelGGL(colsum_kernel, dim3((cs + 255) / 256), dim3(256), 0, st, (const float*)part, nb, cs, out + c0,
-                       accumulate);
+    colred(part, nb, cs, nullptr, out + c0, accumulate, st);
   }
   SM_CHECK_LAUNCH();
   return 0;
