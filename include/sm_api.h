@@ -30,11 +30,15 @@ extern "C" {
  * decoder_pred) and torch TransformerEncoderLayer in_proj/out_proj/linear1/2.
  * C = alpha*op(A)op(B) + bias (+ beta*R, R = C when null); epi bit0 = exact GELU
  * (aux <- pre-activation), bit1 = round the branch to bf16 before adding R (autocast).
+ * Branch regularisers of the training step: elementwise dropout (drop_p, counter-hash
+ * RNG keyed by seed and the element index, nn.Dropout semantics: keep w.p. 1-p, scale
+ * 1/(1-p)) and DropPath (branch *= row_scale[row / rows_per_group]).
  * a_layout 0: A[M][K], 1: A[K][M];  b_layout 0: B[N][K], 1: B[K][N]. */
 int64_t sm_gemm_workspace_bytes(int ab_dtype, int M, int N, int K);
 int sm_gemm(int ab_dtype, int c_dtype, int a_layout, int b_layout, int M, int N, int K,
             const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc,
             const float* bias, float alpha, float beta, int epi, void* aux, const void* R,
+            float drop_p, uint64_t seed, const float* row_scale, int64_t rows_per_group,
             void* workspace, int64_t ws_bytes, hipStream_t stream);
 
 /* ---- fused attention (tiny_vit.py:103 F.scaled_dot_product_attention;
@@ -60,20 +64,30 @@ int64_t sm_bn_workspace_bytes(int64_t M, int C);
 int sm_bn_stats(int x_dtype, int64_t M, int C, const void* x, float* mean, float* rstd,
                 float* run_mean, float* run_var, int64_t* num_batches_tracked, float momentum, float eps,
                 int updates, void* ws, int64_t ws_bytes, hipStream_t st);
+/* y = R + row_scale[row/rows_per_group] * act(BN(x)) (R / row_scale nullable: MBConv
+ * residual with DropPath, tiny_vit.py:53-56) */
 int sm_bn_apply(int x_dtype, int y_dtype, int64_t M, int C, const void* x, const float* mean,
                 const float* rstd, const float* w, const float* b, void* y, int gelu, const void* R,
-                hipStream_t st);
+                const float* row_scale, int64_t rows_per_group, hipStream_t st);
 int sm_bn_bwd(int x_dtype, int g_dtype, int64_t M, int C, const void* dy, const void* x,
               const float* mean, const float* rstd, const float* w, const float* b, int gelu,
-              void* dx, float* dw, float* db, void* ws, int64_t ws_bytes, hipStream_t st);
+              const float* row_scale, int64_t rows_per_group, void* dx, float* dw, float* db, void* ws,
+              int64_t ws_bytes, hipStream_t st);
 
 /* ---- elementwise (GELU tiny_vit.py:44,47,68,80; residual adds; casts) */
-int sm_gelu_bwd(int pre_dtype, int g_dtype, int64_t n, const void* pre, const void* dy, void* dx,
-                hipStream_t st);
+int sm_gelu_bwd(int pre_dtype, int g_dtype, int64_t n, int ncols, const void* pre, const void* dy, void* dx,
+                float drop_p, uint64_t seed, hipStream_t st);
 int sm_add(int a_dtype, int o_dtype, int64_t n, const void* a, const void* b, void* o, hipStream_t st);
 int sm_cast(int a_dtype, int o_dtype, int64_t n, const void* a, void* o, hipStream_t st);
 int sm_fill(float* p, int64_t n, float v, hipStream_t st);
-int sm_gelu_fwd(int dtype, int64_t n, const void* x, void* y, hipStream_t st);
+int sm_gelu_fwd(int dtype, int64_t n, int ncols, const void* x, void* y, float drop_p, uint64_t seed,
+                hipStream_t st);
+/* backward of the branch regularisers: dx = dy * dropout-mask * row_scale[row/rows_per_group]
+ * (nn.Dropout of the decoder layers; timm DropPath of tiny_vit.py:52,114) */
+int sm_dropout_bwd(int dtype, int64_t n, int ncols, const void* dy, void* dx, float drop_p, uint64_t seed,
+                   const float* row_scale, int64_t rows_per_group, hipStream_t st);
+/* DropPath per-sample keep scales: out[i] = keep ? 1/(1-p) : 0 */
+int sm_droppath_scale(int n, float p, uint64_t seed, float* out, hipStream_t st);
 /* column sums (Linear bias gradients): out[c] (+)= sum_m x[m][c] */
 int64_t sm_colsum_workspace_bytes(int64_t M, int C);
 int sm_colsum(int dtype, int64_t M, int C, const void* x, float* out, int accumulate, void* ws,

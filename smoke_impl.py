@@ -29,8 +29,10 @@ def run():
            "ssl": {"mask_ratio": r, "norm_pix_loss": True}}
     clip = torch.from_numpy(synthetic_clip(B, T, S, seed=11))
     for bf16 in (False, True):
+        from ssl_mae_amd import parity_mode
         model = TinyVideoMAE(tiny_vit_21m_variant(img_size=S), cfg)
         apply_rule(model)
+        parity_mode(model)
         model = model.to("cuda:0").train()
         opt = FusedAdamW(model.parameters(), lr=5e-4, weight_decay=0.05)
         torch.manual_seed(42)

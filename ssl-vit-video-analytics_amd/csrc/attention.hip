@@ -100,10 +100,22 @@ SM_DEV bf16x8 acc_to_frag(const f32x16& a, int s) {
 }
 SM_DEV int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
+// dropout mask on the attention probability P[n,hd,q,k]: row (n*H+hd)*L+q, column k
 SM_DEV float drop_keep_scale(const AttnArgs& a, int n, int hd, int q, int k) {
-  // dropout mask on the attention probability P[n,hd,q,k]
-  const uint64_t idx = (((uint64_t)(n * a.H + hd) * a.L + q) * (uint64_t)a.L) + k;
-  return uniform01(a.seed, idx) >= a.drop_p ? 1.0f / (1.0f - a.drop_p) : 0.0f;
+  const uint64_t row = (uint64_t)(n * a.H + hd) * a.L + q;
+  return drop_keep(seed32(a.seed), row, (uint32_t)k, drop_thr(a.drop_p)) ? 1.0f / (1.0f - a.drop_p) : 0.0f;
+}
+
+// Multipliers for the 32 key values a lane holds in a 32x32 accumulator column:
+// keys kb + acc_row(r, h); consecutive keys r, r+1 (r&3 in {0,2}) share one hash.
+SM_DEV void drop_mult_tile(uint32_t rowbase, int kb, int h, int L, uint32_t thr, float ks, float* m) {
+#pragma unroll
+  for (int r = 0; r < 16; r += 2) {
+    const int key = kb + (r & 3) + 8 * (r >> 2) + 4 * h;
+    const uint32_t hv = drop_hash(rowbase, (uint32_t)key);
+    m[r] = (key < L && drop_keep_bits(hv, (uint32_t)key, thr)) ? ks : 0.f;
+    m[r + 1] = (key + 1 < L && drop_keep_bits(hv, (uint32_t)(key + 1), thr)) ? ks : 0.f;
+  }
 }
 
 // =============================================================== bf16 forward
@@ -135,6 +147,9 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16(AttnArgs a) {
     for (int r = 0; r < 16; ++r) o[t][r] = 0.f;
   float m = NEG_BIG, lsum = 0.f;
   const float c = a.scale * LOG2E;
+  const uint32_t drb = drop_rowbase(seed32(a.seed), (uint64_t)(n * a.H + hd) * a.L + q);
+  const uint32_t dthr = drop_thr(a.drop_p);
+  const float dks = DROP ? 1.f / (1.f - a.drop_p) : 1.f;
 
   for (int k0 = 0; k0 < a.L; k0 += KT) {
     __syncthreads();
@@ -151,36 +166,45 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16(AttnArgs a) {
         st[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(lk, 32 * u + (l & 31), s), qf[s],
                                                          st[u], 0, 0, 0);
     }
+    // raw-score max (scale > 0 keeps the argmax); masking only on the ragged tile
     float mt = NEG_BIG;
+    if (k0 + KT > a.L) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (k0 + 32 * u + acc_row(r, h) >= a.L) st[u][r] = NEG_BIG;
+    }
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = k0 + 32 * u + acc_row(r, h);
-        float x = st[u][r] * c;
-        if (key >= a.L) x = NEG_BIG;
-        st[u][r] = x;
-        mt = fmaxf(mt, x);
-      }
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-    const float mn = fmaxf(m, mt);
-    const float alpha = exp2f(m - mn);
+      for (int r = 0; r < 16; ++r) mt = fmaxf(mt, st[u][r]);
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * c;
+    // rescale only when some row's max grew (exact: alpha == 1 otherwise)
+    const bool grow = mt > m;
+    const float mn = grow ? mt : m;
+    const float alpha = grow ? __builtin_amdgcn_exp2f(m - mn) : 1.f;
     m = mn;
     float ps = 0.f;
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < 2; ++u) {
+      float dm[16];
+      if (DROP) drop_mult_tile(drb, k0 + 32 * u, h, a.L, dthr, dks, dm);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float p = exp2f(st[u][r] - mn);
+        float p = __builtin_amdgcn_exp2f(fmaf(st[u][r], c, -mn));
         ps += p;
-        if (DROP) p *= drop_keep_scale(a, n, hd, q, k0 + 32 * u + acc_row(r, h));
+        if (DROP) p *= dm[r];
         st[u][r] = p;
       }
+    }
     lsum = lsum * alpha + ps;
+    if (__any(grow)) {
 #pragma unroll
-    for (int t = 0; t < D / 32; ++t)
+      for (int t = 0; t < D / 32; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+        for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+    }
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -233,7 +257,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(AttnArgs a) {
   constexpr int QT = 64;
   __shared__ __attribute__((aligned(16))) char lq[QT * D * 2];
   __shared__ __attribute__((aligned(16))) char ldo[QT * D * 2];
-  __shared__ float llse[QT], ldel[QT];
+  __shared__ __attribute__((aligned(16))) float llse[QT];
+  __shared__ __attribute__((aligned(16))) float ldel[QT];
   const int n = blockIdx.z, hd = blockIdx.y;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5;
   const int C = a.H * D;
@@ -284,20 +309,47 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(AttnArgs a) {
         sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(lq, 32 * u + (l & 31), s), kf[s], sacc, 0, 0, 0);
         dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(ldo, 32 * u + (l & 31), s), vf[s], dpacc, 0, 0, 0);
       }
-      // rows = queries (regs), column = this lane's key
+      // rows = queries (regs), column = this lane's key.  Row constants come in
+      // as 16-B LDS reads (4 consecutive query rows per register group).
+      float lse4[16], del4[16];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 a4 = *(const float4*)&llse[32 * u + 8 * g + 4 * h];
+        const float4 b4 = *(const float4*)&ldel[32 * u + 8 * g + 4 * h];
+        lse4[4 * g] = a4.x; lse4[4 * g + 1] = a4.y; lse4[4 * g + 2] = a4.z; lse4[4 * g + 3] = a4.w;
+        del4[4 * g] = b4.x; del4[4 * g + 1] = b4.y; del4[4 * g + 2] = b4.z; del4[4 * g + 3] = b4.w;
+      }
+      float dmul[16];
+      if (DROP) {
+        // keys 2j, 2j+1 (lanes l, l^1) share one hash per query row: each lane
+        // hashes every other row and swaps with its partner through DPP.
+        const uint32_t thr = drop_thr(a.drop_p);
+        const float ks = 1.f / (1.f - a.drop_p);
+        const bool odd = key & 1;
+        const uint32_t s32 = seed32(a.seed);
+        const uint64_t rbase = (uint64_t)(n * a.H + hd) * a.L + q0 + 32 * u;
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          const int qi = acc_row(r + (odd ? 1 : 0), h);
+          const uint32_t mine = drop_hash(drop_rowbase(s32, rbase + qi), (uint32_t)key);
+          const uint32_t other = (uint32_t)__builtin_amdgcn_mov_dpp((int)mine, 0xB1, 0xF, 0xF, false);
+          const uint32_t h0 = odd ? other : mine, h1 = odd ? mine : other;   // rows r, r+1
+          const bool v0 = q0 + 32 * u + acc_row(r, h) < a.L, v1 = q0 + 32 * u + acc_row(r + 1, h) < a.L;
+          dmul[r] = (v0 && drop_keep_bits(h0, (uint32_t)key, thr)) ? ks : 0.f;
+          dmul[r + 1] = (v1 && drop_keep_bits(h1, (uint32_t)key, thr)) ? ks : 0.f;
+        }
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int qi = 32 * u + acc_row(r, h);
-        float p = exp2f(sacc[r] * c - llse[qi]);
+        const float p = __builtin_amdgcn_exp2f(fmaf(sacc[r], c, -lse4[r]));
         float dp = dpacc[r];
         if (DROP) {
-          const float ks = (q0 + qi < a.L) ? drop_keep_scale(a, n, hd, q0 + qi, key) : 0.f;
-          dp *= ks;
-          sacc[r] = p * ks;              // dropped P feeds dV
+          dp *= dmul[r];
+          sacc[r] = p * dmul[r];         // dropped P feeds dV
         } else {
           sacc[r] = p;
         }
-        dpacc[r] = p * (dp - ldel[qi]);  // dS
+        dpacc[r] = p * (dp - del4[r]);   // dS
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -362,6 +414,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_bf16(AttnArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) dq[t][r] = 0.f;
   const float c = a.scale * LOG2E;
+  const uint32_t drb = drop_rowbase(seed32(a.seed), (uint64_t)(n * a.H + hd) * a.L + q);
+  const uint32_t dthr = drop_thr(a.drop_p);
+  const float dks = DROP ? 1.f / (1.f - a.drop_p) : 1.f;
 
   for (int k0 = 0; k0 < a.L; k0 += KT) {
     __syncthreads();
@@ -378,12 +433,14 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_bf16(AttnArgs a) {
         sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(lk, 32 * u + (l & 31), s), qf[s], sacc, 0, 0, 0);
         dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(lv, 32 * u + (l & 31), s), df[s], dpacc, 0, 0, 0);
       }
+      float dm[16];
+      if (DROP) drop_mult_tile(drb, k0 + 32 * u, h, a.L, dthr, dks, dm);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int key = k0 + 32 * u + acc_row(r, h);
-        float p = key < a.L ? exp2f(sacc[r] * c - lse2) : 0.f;
+        float p = key < a.L ? __builtin_amdgcn_exp2f(fmaf(sacc[r], c, -lse2)) : 0.f;
         float dp = dpacc[r];
-        if (DROP) dp *= (key < a.L && qok) ? drop_keep_scale(a, n, hd, q, key) : 0.f;
+        if (DROP) dp *= dm[r];
         dpacc[r] = p * (dp - dl);
       }
 #pragma unroll

@@ -98,17 +98,30 @@ SM_DEV float block_sum(float v, float* red) {
 }
 
 // ---------------------------------------------------------------- counter RNG
-// Stateless 32-bit hash (used for dropout / drop-path masks): a keyed
-// splitmix-style mixer of (seed, offset).  Deterministic and replayable in bwd.
-SM_DEV uint32_t mix32(uint64_t seed, uint64_t idx) {
-  uint64_t z = seed * 0x9E3779B97F4A7C15ull + idx + 0x632BE59BD9B4E019ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return (uint32_t)(z >> 32);
+// Dropout / DropPath masks are a pure function of (seed, row, column):
+//   h    = fmix32(seed32 + row * 0x9E3779B1 + (col >> 1) * 0x7FEB352D)
+//   bits = (col & 1) ? h >> 16 : h & 0xFFFF          (one hash per column pair)
+//   keep = bits >= round(p * 65536), kept values scaled by 1/(1-p)
+// so every kernel that touches an element (forward, checkpoint recompute,
+// backward) regenerates the same mask without storing it.  `row` is the tensor
+// row (or the attention row (n*H + h)*L + q); fmix32 is MurmurHash3's finalizer.
+SM_DEV uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
 }
-SM_DEV float uniform01(uint64_t seed, uint64_t idx) {
-  return (mix32(seed, idx) >> 8) * (1.0f / 16777216.0f);
+SM_DEV uint32_t seed32(uint64_t seed) { return (uint32_t)seed ^ (uint32_t)(seed >> 32); }
+SM_DEV uint32_t drop_rowbase(uint32_t s32, uint64_t row) { return s32 + (uint32_t)row * 0x9E3779B1u; }
+SM_DEV uint32_t drop_hash(uint32_t rowbase, uint32_t col) { return fmix32(rowbase + (col >> 1) * 0x7FEB352Du); }
+SM_DEV uint32_t drop_thr(float p) { return (uint32_t)(p * 65536.f + 0.5f); }
+SM_DEV bool drop_keep_bits(uint32_t h, uint32_t col, uint32_t thr) {
+  return ((col & 1) ? (h >> 16) : (h & 0xFFFFu)) >= thr;
+}
+SM_DEV bool drop_keep(uint32_t s32, uint64_t row, uint32_t col, uint32_t thr) {
+  return drop_keep_bits(drop_hash(drop_rowbase(s32, row), col), col, thr);
 }
 
 // Reduce partial slabs part[nb][ncols] over nb.  Block = 32 columns x 8 row groups;

@@ -33,6 +33,10 @@ struct GemmArgs {
   int epi;          // bit0: exact GELU; bit1: round the branch to bf16 before the residual add
   void* aux;        // pre-activation output (same dtype/ld as C) when GELU
   const void* R;    // residual input (dtype/ld of C); null with beta != 0 -> C itself
+  float drop_p;     // dropout on the branch (before the residual add / after GELU)
+  uint64_t seed;
+  const float* row_scale;   // DropPath: branch *= row_scale[row / rows_per_group]
+  int64_t rows_per_group;
   float* partial;   // split-K fp32 slabs [z][M][N] (when non-null: raw store, no epilogue)
 };
 
@@ -47,11 +51,14 @@ SM_DEV void epilogue_store(const GemmArgs& g, int64_t row, int col, float acc) {
   TC* C = (TC*)g.C;
   const int64_t idx = row * g.ldc + col;
   if (g.epi & 2) v = (float)(__bf16)v;   // autocast: the Linear output is bf16 before the fp32 add
-  if (g.beta != 0.f) v += g.beta * to_f<TC>(g.R ? ((const TC*)g.R)[idx] : C[idx]);
   if (g.epi & 1) {
     if (g.aux) ((TC*)g.aux)[idx] = from_f<TC>(v);
     v = gelu_f(v);
   }
+  if (g.drop_p > 0.f)
+    v *= drop_keep(seed32(g.seed), (uint64_t)row, (uint32_t)col, drop_thr(g.drop_p)) ? 1.f / (1.f - g.drop_p) : 0.f;
+  if (g.row_scale) v *= g.row_scale[row / g.rows_per_group];
+  if (g.beta != 0.f) v += g.beta * to_f<TC>(g.R ? ((const TC*)g.R)[idx] : C[idx]);
   C[idx] = from_f<TC>(v);
 }
 
@@ -177,18 +184,85 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
     __syncthreads();
   }
   const int h = l >> 5;
+  if (g.partial || (g.N & 7) || (g.ldc & 7)) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int col = n0 + wn + 32 * j + (l & 31);
-      if (col >= g.N) continue;
+      for (int j = 0; j < 2; ++j) {
+        const int col = n0 + wn + 32 * j + (l & 31);
+        if (col >= g.N) continue;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int64_t row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (row < g.M) epilogue_store<TC>(g, row, col, acc[i][j][r]);
+        }
+      }
+    return;
+  }
+  // Row-vector epilogue: the fp32 accumulators are staged through LDS (half the
+  // tile at a time: rows {32i..32i+31} of each wave row-group), then every thread
+  // finishes 8 consecutive columns of a row: bias, GELU (+aux), dropout (one hash
+  // per column pair), DropPath row scale, residual — all as 16-byte vectors.
+  float* stg = (float*)lds;  // [64][128] fp32 = 32 KB (the operand tiles are dead)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int64_t row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (row < g.M) epilogue_store<TC>(g, row, col, acc[i][j][r]);
+        const int srow = (w >> 1) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        stg[srow * 128 + wn + 32 * j + (l & 31)] = acc[i][j][r];
+      }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int cidx = threadIdx.x + 256 * it;      // 64 rows x 16 chunks
+      const int srow = cidx >> 4, cc = (cidx & 15) * 8;
+      const int64_t row = m0 + (srow >> 5) * 64 + 32 * i + (srow & 31);
+      const int col0 = n0 + cc;
+      if (row < g.M && col0 < g.N) {
+        float v[8];
+        const float4 a0 = *(const float4*)(stg + srow * 128 + cc);
+        const float4 a1 = *(const float4*)(stg + srow * 128 + cc + 4);
+        v[0] = a0.x; v[1] = a0.y; v[2] = a0.z; v[3] = a0.w; v[4] = a1.x; v[5] = a1.y; v[6] = a1.z; v[7] = a1.w;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          v[e] *= g.alpha;
+          if (g.bias) v[e] += g.bias[col0 + e];
+          if (g.epi & 2) v[e] = (float)(__bf16)v[e];
+        }
+        const int64_t idx = row * g.ldc + col0;
+        if (g.epi & 1) {
+          if (g.aux) store8((TC*)g.aux + idx, v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = gelu_f(v[e]);
+        }
+        if (g.drop_p > 0.f) {
+          const uint32_t rb = drop_rowbase(seed32(g.seed), (uint64_t)row), thr = drop_thr(g.drop_p);
+          const float ks = 1.f / (1.f - g.drop_p);
+#pragma unroll
+          for (int e = 0; e < 8; e += 2) {
+            const uint32_t hv = drop_hash(rb, (uint32_t)(col0 + e));
+            v[e] *= drop_keep_bits(hv, (uint32_t)(col0 + e), thr) ? ks : 0.f;
+            v[e + 1] *= drop_keep_bits(hv, (uint32_t)(col0 + e + 1), thr) ? ks : 0.f;
+          }
+        }
+        if (g.row_scale) {
+          const float rs = g.row_scale[row / g.rows_per_group];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] *= rs;
+        }
+        if (g.beta != 0.f) {
+          float rr[8];
+          load8(g.R ? (const TC*)g.R + idx : (const TC*)g.C + idx, rr);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += g.beta * rr[e];
+        }
+        store8((TC*)g.C + idx, v);
       }
     }
+    __syncthreads();
+  }
 }
 
 // ============================================================ f32 MFMA kernel
@@ -306,6 +380,7 @@ extern "C" int64_t sm_gemm_workspace_bytes(int ab_dtype, int M, int N, int K) {
 extern "C" int sm_gemm(int ab_dtype, int c_dtype, int a_layout, int b_layout, int M, int N, int K,
                        const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc,
                        const float* bias, float alpha, float beta, int epi, void* aux, const void* R,
+                       float drop_p, uint64_t seed, const float* row_scale, int64_t rows_per_group,
                        void* workspace, int64_t ws_bytes, hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
   if (ab_dtype == SM_BF16) {
@@ -317,6 +392,7 @@ extern "C" int sm_gemm(int ab_dtype, int c_dtype, int a_layout, int b_layout, in
   GemmArgs g{};
   g.M = M; g.N = N; g.K = K; g.A = A; g.lda = lda; g.B = B; g.ldb = ldb; g.C = C; g.ldc = ldc;
   g.bias = bias; g.alpha = alpha; g.beta = beta; g.epi = epi; g.aux = aux; g.R = R;
+  g.drop_p = drop_p; g.seed = seed; g.row_scale = row_scale; g.rows_per_group = rows_per_group > 0 ? rows_per_group : 1;
   int splits = choose_splits(M, N, K, ab_dtype == SM_BF16);
   if (splits > 1 && (workspace == nullptr || ws_bytes < (int64_t)splits * M * N * 4)) splits = 1;
   const int bk = ab_dtype == SM_BF16 ? BKT : FBK;

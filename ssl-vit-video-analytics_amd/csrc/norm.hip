@@ -233,7 +233,8 @@ struct Col8 {
 template <typename TI, typename TO>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const TI* x, const float* mean, const float* rstd,
                                                        const float* w, const float* b, TO* y, int64_t M, int C,
-                                                       int rows_per_block, int gelu, const TO* R) {
+                                                       int rows_per_block, int gelu, const TO* R,
+                                                       const float* row_scale, int64_t rpg) {
   Col8 cm(C);
   if (!cm.active()) return;
   float sc[8], sh[8];
@@ -254,6 +255,11 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const TI* x, const float*
       const float t = v[j] * sc[j] + sh[j];
       v[j] = gelu ? gelu_f(t) : t;
     }
+    if (row_scale) {
+      const float rs = row_scale[row / rpg];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] *= rs;
+    }
     if (R) {
       float rr[8];
       load8(R + e, rr);
@@ -269,7 +275,7 @@ template <typename TI, typename TD>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const TD* dy, const TI* x, const float* mean,
                                                             const float* rstd, const float* w, const float* b,
                                                             int64_t M, int C, int rows_per_block, int gelu,
-                                                            float* part) {
+                                                            const float* row_scale, int64_t rpg, float* part) {
   __shared__ float red[2][256 * 4];
   ColMap cm(C);
   float sg[4] = {0, 0, 0, 0}, sgx[4] = {0, 0, 0, 0};
@@ -286,10 +292,11 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const TD* dy, const 
       float xv[4], dv[4];
       load4(x + row * C + cm.chunk * 4, xv);
       load4(dy + row * C + cm.chunk * 4, dv);
+      const float rsc = row_scale ? row_scale[row / rpg] : 1.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float xh = (xv[j] - mu[j]) * rs[j];
-        float gg = dv[j];
+        float gg = dv[j] * rsc;
         if (gelu) gg *= gelu_grad(xh * ww[j] + bb[j]);
         sg[j] += gg;
         sgx[j] += gg * xh;
@@ -328,7 +335,8 @@ template <typename TI, typename TD, typename TX>
 __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const TD* dy, const TI* x, const float* mean,
                                                         const float* rstd, const float* w, const float* b,
                                                         const float* coef, TX* dx, int64_t M, int C,
-                                                        int rows_per_block, int gelu) {
+                                                        int rows_per_block, int gelu, const float* row_scale,
+                                                        int64_t rpg) {
   Col8 cm(C);
   if (!cm.active()) return;
   float mu[8], rs[8], ww[8], bb[8], k0[8], k1[8];
@@ -345,10 +353,11 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const TD* dy, const TI* 
     float xv[8], dv[8], o[8];
     load8(x + e, xv);
     load8(dy + e, dv);
+    const float rsc = row_scale ? row_scale[row / rpg] : 1.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float xh = (xv[j] - mu[j]) * rs[j];
-      float gg = dv[j];
+      float gg = dv[j] * rsc;
       if (gelu) gg *= gelu_grad(xh * ww[j] + bb[j]);
       o[j] = ww[j] * rs[j] * (gg - k0[j] - xh * k1[j]);
     }
@@ -357,17 +366,55 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const TD* dy, const TI* 
 }
 
 // ============================================================ elementwise
+// 8 consecutive elements of one row (ncols % 8 == 0): dropout multipliers
+SM_DEV void drop_mult8(int64_t e, int ncols, float drop_p, uint64_t seed, float* m) {
+  const float ks = 1.f / (1.f - drop_p);
+  const int64_t row = e / ncols;
+  const uint32_t c0 = (uint32_t)(e - row * ncols);
+  const uint32_t rb = drop_rowbase(seed32(seed), (uint64_t)row), thr = drop_thr(drop_p);
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) {
+    const uint32_t h = drop_hash(rb, c0 + j);
+    m[j] = drop_keep_bits(h, c0 + j, thr) ? ks : 0.f;
+    m[j + 1] = drop_keep_bits(h, c0 + j + 1, thr) ? ks : 0.f;
+  }
+}
+
 template <typename T, typename TG>
-__global__ void gelu_bwd_kernel(const T* pre, const TG* dy, TG* dx, int64_t total8) {
+__global__ void gelu_bwd_kernel(const T* pre, const TG* dy, TG* dx, int64_t total8, int ncols, float drop_p,
+                                uint64_t seed) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total8;
        i += (int64_t)gridDim.x * blockDim.x) {
-    float p[8], d[8];
+    float p[8], d[8], m[8];
     load8(pre + i * 8, p);
     load8(dy + i * 8, d);
+    if (drop_p > 0.f) drop_mult8(i * 8, ncols, drop_p, seed, m);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) d[j] *= gelu_grad(p[j]);
+    for (int j = 0; j < 8; ++j) d[j] *= (drop_p > 0.f ? m[j] : 1.f) * gelu_grad(p[j]);
     store8(dx + i * 8, d);
   }
+}
+
+// dx = dy * dropout_mask * row_scale[row / rpg]   (backward of the branch regularisers)
+template <typename T>
+__global__ void dropout_bwd_kernel(const T* dy, T* dx, int64_t total8, int ncols, float drop_p, uint64_t seed,
+                                   const float* row_scale, int64_t rpg) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total8;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float d[8], m[8];
+    load8(dy + i * 8, d);
+    const int64_t e = i * 8;
+    const float rs = row_scale ? row_scale[(e / ncols) / rpg] : 1.f;
+    if (drop_p > 0.f) drop_mult8(e, ncols, drop_p, seed, m);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] *= rs * (drop_p > 0.f ? m[j] : 1.f);
+    store8(dx + i * 8, d);
+  }
+}
+
+__global__ void droppath_scale_kernel(int n, float p, uint64_t seed, float* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = drop_keep(seed32(seed), (uint64_t)i, 0u, drop_thr(p)) ? 1.f / (1.f - p) : 0.f;
 }
 
 template <typename TA, typename TB, typename TO>
@@ -394,13 +441,14 @@ __global__ void cast_kernel(const TA* a, TO* o, int64_t total8) {
 }
 
 template <typename T>
-__global__ void gelu_fwd_kernel(const T* x, T* y, int64_t total8) {
+__global__ void gelu_fwd_kernel(const T* x, T* y, int64_t total8, int ncols, float drop_p, uint64_t seed) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total8;
        i += (int64_t)gridDim.x * blockDim.x) {
-    float v[8];
+    float v[8], m[8];
     load8(x + i * 8, v);
+    if (drop_p > 0.f) drop_mult8(i * 8, ncols, drop_p, seed, m);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = gelu_f(v[j]);
+    for (int j = 0; j < 8; ++j) v[j] = gelu_f(v[j]) * (drop_p > 0.f ? m[j] : 1.f);
     store8(y + i * 8, v);
   }
 }
@@ -538,21 +586,24 @@ extern "C" int sm_bn_stats(int x_dtype, int64_t M, int C, const void* x, float* 
 
 extern "C" int sm_bn_apply(int x_dtype, int y_dtype, int64_t M, int C, const void* x, const float* mean,
                            const float* rstd, const float* w, const float* b, void* y, int gelu,
-                           const void* R, hipStream_t st) {
+                           const void* R, const float* row_scale, int64_t rows_per_group, hipStream_t st) {
   if (M <= 0) return 0;
   if (C % 8 || C / 8 > 256) return -2;
   const int rpb = stream_rows_per_block(M);
   const int nb = (int)((M + rpb - 1) / rpb);
   DISPATCH2(x_dtype, y_dtype,
             hipLaunchKernelGGL((bn_apply_kernel<T1, T2>), dim3(nb), dim3(256), 0, st, (const T1*)x,
-                               mean, rstd, w, b, (T2*)y, M, C, rpb, gelu, (const T2*)R));
+                               mean, rstd, w, b, (T2*)y, M, C, rpb, gelu, (const T2*)R, row_scale,
+                               rows_per_group > 0 ? rows_per_group : 1));
   SM_CHECK_LAUNCH();
   return 0;
 }
 
 extern "C" int sm_bn_bwd(int x_dtype, int g_dtype, int64_t M, int C, const void* dy, const void* x,
                          const float* mean, const float* rstd, const float* w, const float* b, int gelu,
-                         void* dx, float* dw, float* db, void* ws, int64_t ws_bytes, hipStream_t st) {
+                         const float* row_scale, int64_t rows_per_group, void* dx, float* dw, float* db, void* ws,
+                         int64_t ws_bytes, hipStream_t st) {
+  const int64_t rpg = rows_per_group > 0 ? rows_per_group : 1;
   if (M <= 0) return 0;
   if (C % 8 || C / 4 > 256) return -2;
   const int rpb = red_rows_per_block(M, C);
@@ -563,25 +614,26 @@ extern "C" int sm_bn_bwd(int x_dtype, int g_dtype, int64_t M, int C, const void*
   float* coef = (float*)(sums + 2 * C);
   DISPATCH2(x_dtype, g_dtype,
             hipLaunchKernelGGL((bn_bwd_reduce_kernel<T1, T2>), dim3(nb), dim3(256), 0, st, (const T2*)dy,
-                               (const T1*)x, mean, rstd, w, b, M, C, rpb, gelu, part));
+                               (const T1*)x, mean, rstd, w, b, M, C, rpb, gelu, row_scale, rpg, part));
   colred(part, nb, 2 * C, sums, nullptr, 0, st);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 127) / 128), dim3(128), 0, st, sums, M, C, dw, db, coef);
   const int srpb = stream_rows_per_block(M);
   const int snb = (int)((M + srpb - 1) / srpb);
   DISPATCH2(x_dtype, g_dtype,
             hipLaunchKernelGGL((bn_bwd_dx_kernel<T1, T2, T2>), dim3(snb), dim3(256), 0, st,
-                               (const T2*)dy, (const T1*)x, mean, rstd, w, b, coef, (T2*)dx, M, C, srpb, gelu));
+                               (const T2*)dy, (const T1*)x, mean, rstd, w, b, coef, (T2*)dx, M, C, srpb, gelu,
+                               row_scale, rpg));
   SM_CHECK_LAUNCH();
   return 0;
 }
 
-extern "C" int sm_gelu_bwd(int pre_dtype, int g_dtype, int64_t n, const void* pre, const void* dy, void* dx,
-                           hipStream_t st) {
+extern "C" int sm_gelu_bwd(int pre_dtype, int g_dtype, int64_t n, int ncols, const void* pre, const void* dy,
+                           void* dx, float drop_p, uint64_t seed, hipStream_t st) {
   if (n <= 0) return 0;
   if (n % 8) return -2;
   DISPATCH2(pre_dtype, g_dtype,
             hipLaunchKernelGGL((gelu_bwd_kernel<T1, T2>), dim3(ew_blocks(n / 8)), dim3(256), 0, st,
-                               (const T1*)pre, (const T2*)dy, (T2*)dx, n / 8));
+                               (const T1*)pre, (const T2*)dy, (T2*)dx, n / 8, ncols, drop_p, seed));
   SM_CHECK_LAUNCH();
   return 0;
 }
@@ -637,13 +689,38 @@ extern "C" int sm_colsum(int dtype, int64_t M, int C, const void* x, float* out,
   return 0;
 }
 
-extern "C" int sm_gelu_fwd(int dtype, int64_t n, const void* x, void* y, hipStream_t st) {
+extern "C" int sm_gelu_fwd(int dtype, int64_t n, int ncols, const void* x, void* y, float drop_p, uint64_t seed,
+                           hipStream_t st) {
   if (n <= 0) return 0;
   if (n % 8) return -2;
   if (dtype == SM_BF16)
-    hipLaunchKernelGGL(gelu_fwd_kernel<__bf16>, dim3(ew_blocks(n / 8)), dim3(256), 0, st, (const __bf16*)x, (__bf16*)y, n / 8);
+    hipLaunchKernelGGL(gelu_fwd_kernel<__bf16>, dim3(ew_blocks(n / 8)), dim3(256), 0, st, (const __bf16*)x,
+                       (__bf16*)y, n / 8, ncols, drop_p, seed);
   else
-    hipLaunchKernelGGL(gelu_fwd_kernel<float>, dim3(ew_blocks(n / 8)), dim3(256), 0, st, (const float*)x, (float*)y, n / 8);
+    hipLaunchKernelGGL(gelu_fwd_kernel<float>, dim3(ew_blocks(n / 8)), dim3(256), 0, st, (const float*)x, (float*)y,
+                       n / 8, ncols, drop_p, seed);
+  SM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int sm_dropout_bwd(int dtype, int64_t n, int ncols, const void* dy, void* dx, float drop_p, uint64_t seed,
+                              const float* row_scale, int64_t rows_per_group, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (n % 8 || ncols % 8) return -2;
+  const int64_t rpg = rows_per_group > 0 ? rows_per_group : 1;
+  if (dtype == SM_BF16)
+    hipLaunchKernelGGL(dropout_bwd_kernel<__bf16>, dim3(ew_blocks(n / 8)), dim3(256), 0, st, (const __bf16*)dy,
+                       (__bf16*)dx, n / 8, ncols, drop_p, seed, row_scale, rpg);
+  else
+    hipLaunchKernelGGL(dropout_bwd_kernel<float>, dim3(ew_blocks(n / 8)), dim3(256), 0, st, (const float*)dy,
+                       (float*)dx, n / 8, ncols, drop_p, seed, row_scale, rpg);
+  SM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int sm_droppath_scale(int n, float p, uint64_t seed, float* out, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(droppath_scale_kernel, dim3((n + 255) / 256), dim3(256), 0, st, n, p, seed, out);
   SM_CHECK_LAUNCH();
   return 0;
 }

@@ -3,3 +3,18 @@ lzc452/SSL-VIT-VIDEO-ANALYTICS: HIP kernels behind a C ABI (libsslmae.so) with a
 host mirror of the reference's module API (tiny_vit_21m_variant, TinyVideoMAE,
 get_tube_mask, patchify, train_one_epoch)."""
 __version__ = "0.1.0"
+
+
+def parity_mode(model):
+    """Disable every stochastic regulariser (decoder Dropout/attention dropout, encoder
+    DropPath) while keeping train-mode BatchNorm — the configuration the golden
+    fixtures were recorded in."""
+    import torch.nn as nn
+    for m in model.modules():
+        if isinstance(m, nn.Dropout):
+            m.p = 0.0
+        if isinstance(m, nn.MultiheadAttention):
+            m.dropout = 0.0
+        if hasattr(m, "drop_prob"):
+            m.drop_prob = 0.0
+    return model

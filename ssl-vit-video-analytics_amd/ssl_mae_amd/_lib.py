@@ -24,7 +24,8 @@ _c_p = ctypes.c_void_p
 _SIGS = {
     "sm_gemm_workspace_bytes": (_c_i64, [_c_i32, _c_i32, _c_i32, _c_i32]),
     "sm_gemm": (_c_i32, [_c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_i64, _c_p, _c_i64,
-                         _c_p, _c_i64, _c_p, _c_f32, _c_f32, _c_i32, _c_p, _c_p, _c_p, _c_i64, _c_p]),
+                         _c_p, _c_i64, _c_p, _c_f32, _c_f32, _c_i32, _c_p, _c_p, _c_f32, _c_u64, _c_p, _c_i64,
+                         _c_p, _c_i64, _c_p]),
     "sm_attn_fwd": (_c_i32, [_c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_f32, _c_f32, _c_u64,
                              _c_p]),
     "sm_attn_bwd": (_c_i32, [_c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_f32,
@@ -38,14 +39,16 @@ _SIGS = {
     "sm_bn_stats": (_c_i32, [_c_i32, _c_i64, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_f32, _c_i32,
                              _c_p, _c_i64, _c_p]),
     "sm_bn_apply": (_c_i32, [_c_i32, _c_i32, _c_i64, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_p,
-                             _c_p]),
-    "sm_bn_bwd": (_c_i32, [_c_i32, _c_i32, _c_i64, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_p,
-                           _c_p, _c_p, _c_i64, _c_p]),
-    "sm_gelu_bwd": (_c_i32, [_c_i32, _c_i32, _c_i64, _c_p, _c_p, _c_p, _c_p]),
+                             _c_p, _c_i64, _c_p]),
+    "sm_bn_bwd": (_c_i32, [_c_i32, _c_i32, _c_i64, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_i64,
+                           _c_p, _c_p, _c_p, _c_p, _c_i64, _c_p]),
+    "sm_gelu_bwd": (_c_i32, [_c_i32, _c_i32, _c_i64, _c_i32, _c_p, _c_p, _c_p, _c_f32, _c_u64, _c_p]),
+    "sm_dropout_bwd": (_c_i32, [_c_i32, _c_i64, _c_i32, _c_p, _c_p, _c_f32, _c_u64, _c_p, _c_i64, _c_p]),
+    "sm_droppath_scale": (_c_i32, [_c_i32, _c_f32, _c_u64, _c_p, _c_p]),
     "sm_add": (_c_i32, [_c_i32, _c_i32, _c_i64, _c_p, _c_p, _c_p, _c_p]),
     "sm_cast": (_c_i32, [_c_i32, _c_i32, _c_i64, _c_p, _c_p, _c_p]),
     "sm_fill": (_c_i32, [_c_p, _c_i64, _c_f32, _c_p]),
-    "sm_gelu_fwd": (_c_i32, [_c_i32, _c_i64, _c_p, _c_p, _c_p]),
+    "sm_gelu_fwd": (_c_i32, [_c_i32, _c_i64, _c_i32, _c_p, _c_p, _c_f32, _c_u64, _c_p]),
     "sm_colsum_workspace_bytes": (_c_i64, [_c_i64, _c_i32]),
     "sm_colsum": (_c_i32, [_c_i32, _c_i64, _c_i32, _c_p, _c_p, _c_i32, _c_p, _c_i64, _c_p]),
     "sm_se_scale": (_c_i32, [_c_i32, _c_p, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p]),

@@ -24,11 +24,28 @@ from . import kernels as K
 
 
 class Mode:
-    __slots__ = ("bf16", "act")
+    """Per-forward execution mode: precision and the base of the counter-hash RNG
+    (dropout / DropPath masks are a pure function of (seed, element index), so the
+    checkpoint recompute and the backward regenerate exactly the forward's masks)."""
+    __slots__ = ("bf16", "act", "seed_base")
 
-    def __init__(self, bf16):
+    def __init__(self, bf16, seed_base=0):
         self.bf16 = bool(bf16)
         self.act = torch.bfloat16 if bf16 else torch.float32
+        self.seed_base = int(seed_base)
+
+    def seed(self, module_index, site):
+        return splitmix64(self.seed_base ^ splitmix64((module_index << 8) | site))
+
+
+_M64 = (1 << 64) - 1
+
+
+def splitmix64(x):
+    x = (x + 0x9E3779B97F4A7C15) & _M64
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & _M64
+    return x ^ (x >> 31)
 
 
 def W(p, mode):
@@ -132,7 +149,11 @@ class MBConvFn(torch.autograd.Function):
         del h2
         a3 = K.linear(h3, W(w_proj, mode).view(Cout, mid))
         del h3
-        out, m5, r5 = _bn_forward(a3, st.bn5, gelu=False, residual=x2d if st.res else None)
+        mean5, rstd5 = K.bn_stats(a3, st.bn5.running_mean, st.bn5.running_var, st.bn5.momentum, st.bn5.eps, 1,
+                                  st.bn5.num_batches_tracked)
+        out = K.bn_apply(a3, mean5, rstd5, g5.detach(), b5.detach(), residual=x2d if st.res else None,
+                         row_scale=st.dp_scale, rows_per_group=Ho * Wo)
+        m5, r5 = mean5, rstd5
         ctx.st = st
         ctx.geom = (Fr, H, Wd, Cin, Ho, Wo)
         ctx.params = (w_exp, g0, b0, w_dw, g2, b2, w_fc0, w_fc2, w_proj, g5, b5)
@@ -149,7 +170,8 @@ class MBConvFn(torch.autograd.Function):
         mid, Cout, s = st.mid, st.cout, st.stride
         _touch(*ctx.params)
         dout2d = dout.reshape(-1, Cout).to(mode.act).contiguous()
-        da3 = K.bn_bwd(dout2d, a3, m5, r5, g5.detach(), b5.detach(), False, G(g5), G(b5))
+        da3 = K.bn_bwd(dout2d, a3, m5, r5, g5.detach(), b5.detach(), False, G(g5), G(b5),
+                       row_scale=st.dp_scale, rows_per_group=Ho * Wo)
         h2 = K.bn_apply(a2, m2, r2, g2.detach(), b2.detach(), gelu=True)
         h3 = K.se_scale(h2, gate, Fr, Ho * Wo, mid)
         K.linear_dw(da3, h3, G(w_proj).view(Cout, mid))
@@ -191,12 +213,14 @@ class BlockFn(torch.autograd.Function):
         ln1, mu1, rs1 = K.layernorm(x, ln1w.detach(), ln1b.detach(), out_dtype=act, eps=st.eps)
         qkv = K.linear(ln1, W(wqkv, mode), bqkv.detach())
         del ln1
-        o, lse = K.attn_fwd(qkv, N, L, H, D, st.attn_drop, st.seed)
-        x2 = K.linear(o, W(wproj, mode), bproj.detach(), out_dtype=x.dtype, residual=x, round_branch=rb)
+        o, lse = K.attn_fwd(qkv, N, L, H, D, st.attn_drop, st.seed_attn)
+        x2 = K.linear(o, W(wproj, mode), bproj.detach(), out_dtype=x.dtype, residual=x, round_branch=rb,
+                      drop_p=st.drop1, seed=st.seed1, row_scale=st.dp1, rows_per_group=L)
         ln2, mu2, rs2 = K.layernorm(x2, ln2w.detach(), ln2b.detach(), out_dtype=act, eps=st.eps)
-        h, hpre = K.linear(ln2, W(w1, mode), b1.detach(), gelu=True)
+        h, hpre = K.linear(ln2, W(w1, mode), b1.detach(), gelu=True, drop_p=st.drop_ff, seed=st.seed_ff)
         del ln2
-        out = K.linear(h, W(w2, mode), b2.detach(), out_dtype=x.dtype, residual=x2, round_branch=rb)
+        out = K.linear(h, W(w2, mode), b2.detach(), out_dtype=x.dtype, residual=x2, round_branch=rb,
+                       drop_p=st.drop2, seed=st.seed2, row_scale=st.dp2, rows_per_group=L)
         del h
         ctx.st = st
         ctx.params = (ln1w, ln1b, wqkv, bqkv, wproj, bproj, ln2w, ln2b, w1, b1, w2, b2)
@@ -216,13 +240,15 @@ class BlockFn(torch.autograd.Function):
         if dout.dtype != x.dtype:
             dout = dout.to(x.dtype)
         db = dout if dout.dtype == act else K.cast(dout, act)       # grad of the bf16 branch
-        h = K.gelu(hpre)
+        if st.drop2 > 0 or st.dp2 is not None:
+            db = K.dropout_bwd(db, st.drop2, st.seed2, st.dp2, L)
+        h = K.gelu(hpre, st.drop_ff, st.seed_ff)
         K.linear_dw(db, h, G(w2))
         K.colsum(db, G(b2))
         del h
         dh = K.linear_dx(db, W(w2, mode))
         del db
-        dhpre = K.gelu_bwd(hpre, dh)
+        dhpre = K.gelu_bwd(hpre, dh, st.drop_ff, st.seed_ff)
         del dh
         ln2 = K.layernorm(x2, ln2w.detach(), ln2b.detach(), out_dtype=act, eps=st.eps)[0]
         K.linear_dw(dhpre, ln2, G(w1))
@@ -233,11 +259,13 @@ class BlockFn(torch.autograd.Function):
         dx2 = K.layernorm_bwd(dln2, x2, mu2, rs2, ln2w.detach(), G(ln2w), G(ln2b), dres=dout)
         del dln2
         dxb = dx2 if dx2.dtype == act else K.cast(dx2, act)
+        if st.drop1 > 0 or st.dp1 is not None:
+            dxb = K.dropout_bwd(dxb, st.drop1, st.seed1, st.dp1, L)
         K.linear_dw(dxb, o, G(wproj))
         K.colsum(dxb, G(bproj))
         do = K.linear_dx(dxb, W(wproj, mode))
         del dxb
-        dqkv = K.attn_bwd(qkv, o, do, lse, N, L, H, D, st.attn_drop, st.seed)
+        dqkv = K.attn_bwd(qkv, o, do, lse, N, L, H, D, st.attn_drop, st.seed_attn)
         del do
         ln1 = K.layernorm(x, ln1w.detach(), ln1b.detach(), out_dtype=act, eps=st.eps)[0]
         K.linear_dw(dqkv, ln1, G(wqkv))

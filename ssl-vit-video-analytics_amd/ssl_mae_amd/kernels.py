@@ -24,7 +24,7 @@ def _ws(nbytes, device):
 
 # ------------------------------------------------------------------ GEMM
 def gemm(A, B, C, M, N, K, a_layout, b_layout, lda, ldb, ldc, bias=None, alpha=1.0, beta=0.0,
-         gelu=False, aux=None, R=None, round_branch=False):
+         gelu=False, aux=None, R=None, round_branch=False, drop_p=0.0, seed=0, row_scale=None, rows_per_group=1):
     _chk(A, B, C)
     ab = dt(A)
     if dt(B) != ab:
@@ -33,18 +33,21 @@ def gemm(A, B, C, M, N, K, a_layout, b_layout, lda, ldb, ldc, bias=None, alpha=1
     ws = _ws(nbytes, A.device) if nbytes else None
     epi = (1 if gelu else 0) | (2 if round_branch else 0)
     call("sm_gemm", ab, dt(C), a_layout, b_layout, M, N, K, ptr(A), lda, ptr(B), ldb, ptr(C), ldc, ptr(bias),
-         float(alpha), float(beta), epi, ptr(aux), ptr(R), ptr(ws), nbytes, stream())
+         float(alpha), float(beta), epi, ptr(aux), ptr(R), float(drop_p), int(seed) & ((1 << 64) - 1), ptr(row_scale),
+         int(rows_per_group), ptr(ws), nbytes, stream())
     return C
 
 
-def linear(x, w, bias=None, out_dtype=None, gelu=False, residual=None, round_branch=False):
-    """y = x @ w^T + bias (+ residual) (GELU optional, returns (y, pre) then)."""
+def linear(x, w, bias=None, out_dtype=None, gelu=False, residual=None, round_branch=False, drop_p=0.0, seed=0,
+           row_scale=None, rows_per_group=1):
+    """y = residual + rs[row] * drop(act(x @ w^T + bias)); returns (y, pre-activation) with GELU."""
     M, K = x.shape
     N = w.shape[0]
     out = torch.empty((M, N), dtype=out_dtype or x.dtype, device=x.device)
     pre = torch.empty_like(out) if gelu else None
     gemm(x, w, out, M, N, K, 0, 0, K, K, N, bias=bias, gelu=gelu, aux=pre,
-         beta=1.0 if residual is not None else 0.0, R=residual, round_branch=round_branch)
+         beta=1.0 if residual is not None else 0.0, R=residual, round_branch=round_branch, drop_p=drop_p,
+         seed=seed, row_scale=row_scale, rows_per_group=rows_per_group)
     return (out, pre) if gelu else out
 
 
@@ -131,35 +134,50 @@ def bn_stats(x2d, running_mean=None, running_var=None, momentum=0.1, eps=1e-5, u
     return mean, rstd
 
 
-def bn_apply(x2d, mean, rstd, w, b, gelu=False, out_dtype=None, residual=None):
+def bn_apply(x2d, mean, rstd, w, b, gelu=False, out_dtype=None, residual=None, row_scale=None, rows_per_group=1):
     M, C = x2d.shape
     y = torch.empty((M, C), dtype=out_dtype or x2d.dtype, device=x2d.device)
     call("sm_bn_apply", dt(x2d), dt(y), M, C, ptr(x2d), ptr(mean), ptr(rstd), ptr(w), ptr(b), ptr(y),
-         1 if gelu else 0, ptr(residual), stream())
+         1 if gelu else 0, ptr(residual), ptr(row_scale), int(rows_per_group), stream())
     return y
 
 
-def bn_bwd(dy, x2d, mean, rstd, w, b, gelu, dw_sink, db_sink):
+def bn_bwd(dy, x2d, mean, rstd, w, b, gelu, dw_sink, db_sink, row_scale=None, rows_per_group=1):
     M, C = x2d.shape
     dx = torch.empty_like(dy)
     nbytes = query("sm_bn_workspace_bytes", M, C)
     ws = _ws(nbytes, x2d.device)
     call("sm_bn_bwd", dt(x2d), dt(dy), M, C, ptr(dy), ptr(x2d), ptr(mean), ptr(rstd), ptr(w), ptr(b),
-         1 if gelu else 0, ptr(dx), ptr(dw_sink), ptr(db_sink), ptr(ws), nbytes, stream())
+         1 if gelu else 0, ptr(row_scale), int(rows_per_group), ptr(dx), ptr(dw_sink), ptr(db_sink), ptr(ws),
+         nbytes, stream())
     return dx
 
 
 # ------------------------------------------------------------------ elementwise
-def gelu(x):
+def gelu(x, drop_p=0.0, seed=0):
     y = torch.empty_like(x)
-    call("sm_gelu_fwd", dt(x), x.numel(), ptr(x), ptr(y), stream())
+    call("sm_gelu_fwd", dt(x), x.numel(), x.shape[-1], ptr(x), ptr(y), float(drop_p), int(seed), stream())
     return y
 
 
-def gelu_bwd(pre, dy):
+def gelu_bwd(pre, dy, drop_p=0.0, seed=0):
     dx = torch.empty_like(dy)
-    call("sm_gelu_bwd", dt(pre), dt(dy), dy.numel(), ptr(pre), ptr(dy), ptr(dx), stream())
+    call("sm_gelu_bwd", dt(pre), dt(dy), dy.numel(), dy.shape[-1], ptr(pre), ptr(dy), ptr(dx), float(drop_p),
+         int(seed), stream())
     return dx
+
+
+def dropout_bwd(dy, drop_p=0.0, seed=0, row_scale=None, rows_per_group=1):
+    dx = torch.empty_like(dy)
+    call("sm_dropout_bwd", dt(dy), dy.numel(), dy.shape[-1], ptr(dy), ptr(dx), float(drop_p), int(seed),
+         ptr(row_scale), int(rows_per_group), stream())
+    return dx
+
+
+def droppath_scale(n, p, seed, device):
+    out = torch.empty(n, dtype=torch.float32, device=device)
+    call("sm_droppath_scale", int(n), float(p), int(seed), ptr(out), stream())
+    return out
 
 
 def add(a, b, out_dtype=None):

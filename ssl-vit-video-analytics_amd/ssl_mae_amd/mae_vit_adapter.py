@@ -22,6 +22,18 @@ def _trunc_normal_(t, std=0.02):
     return nn.init.trunc_normal_(t, 0.0, std, -2.0, 2.0)
 
 
+def next_seed_base(root):
+    """Fresh RNG base per forward: the device generator's seed (set_seed seeds it)
+    plus a per-model forward counter.  The host generator — which drives the tube
+    mask exactly as in the reference — is not consumed."""
+    cnt = getattr(root, "_sm_fwd_count", 0)
+    root._sm_fwd_count = cnt + 1
+    dev = torch.cuda.current_device()
+    base = torch.cuda.default_generators[dev].initial_seed()
+    from .functions import splitmix64
+    return splitmix64((base << 20) ^ cnt)
+
+
 def ensure_flat(root: nn.Module, mode: Mode):
     """Move every parameter of `root` into one flat device buffer (once), then
     mark the start of a forward (zero-on-first-backward, bf16 shadow refresh)."""
@@ -73,6 +85,8 @@ class TinyVideoMAE(nn.Module):
         self.decoder_pred = nn.Linear(self.decoder_embed_dim, self.patch_size ** 2 * 3, bias=True)
         self._mae = True
         self.initialize_weights()
+        from .tiny_vit import index_modules
+        index_modules(self)
 
     def initialize_weights(self):
         _trunc_normal_(self.temporal_pos_embed, std=0.02)
@@ -92,7 +106,7 @@ class TinyVideoMAE(nn.Module):
     def forward(self, x, mask):
         """x [B,3,T,H,W] fp32, mask bool [B,T,L] (True = masked) -> pred [B, T*L, 192]."""
         B, C, T, H, W = x.shape
-        mode = Mode(torch.is_autocast_enabled("cuda"))
+        mode = Mode(torch.is_autocast_enabled("cuda"), next_seed_base(self))
         ensure_flat(self, mode)
         dev = self.mask_token.device
         if x.device != dev:
@@ -114,8 +128,14 @@ class TinyVideoMAE(nn.Module):
                               self.temporal_pos_embed, self.spatial_pos_embed, self.mask_token)
         for layer in self.decoder_blocks.layers:
             sa = layer.self_attn
+            tr = self.training
+            idx = getattr(layer, "_sm_index", 0)
             bst = _St(mode=mode, N=B, L=T * L, heads=self.decoder_num_heads, head_dim=D // self.decoder_num_heads,
-                      eps=layer.norm1.eps, attn_drop=0.0, seed=0)
+                      eps=layer.norm1.eps,
+                      attn_drop=sa.dropout if tr else 0.0, seed_attn=mode.seed(idx, 0),
+                      drop1=layer.dropout1.p if tr else 0.0, seed1=mode.seed(idx, 1),
+                      drop_ff=layer.dropout.p if tr else 0.0, seed_ff=mode.seed(idx, 2),
+                      drop2=layer.dropout2.p if tr else 0.0, seed2=mode.seed(idx, 3), dp1=None, dp2=None)
             xd = BlockFn.apply(xd, bst, layer.norm1.weight, layer.norm1.bias, sa.in_proj_weight, sa.in_proj_bias,
                                sa.out_proj.weight, sa.out_proj.bias, layer.norm2.weight, layer.norm2.bias,
                                layer.linear1.weight, layer.linear1.bias, layer.linear2.weight,

@@ -13,15 +13,27 @@ import torch
 import torch.nn as nn
 import torch.utils.checkpoint as checkpoint
 
+from . import kernels as K
 from .functions import BlockFn, MBConvFn, Mode, StemFn
 
 
 class DropPath(nn.Module):
-    """Stochastic depth placeholder with timm's attribute name (drop_prob)."""
+    """Stochastic depth (timm.layers.DropPath semantics: per-sample keep with
+    probability 1-p, kept samples scaled by 1/(1-p)); applied inside the fused
+    kernels as a per-row-group scale of the residual branch."""
 
     def __init__(self, drop_prob=0.0):
         super().__init__()
         self.drop_prob = drop_prob
+
+
+def droppath_scale(module, n_samples, mode, site, device):
+    """Per-sample branch scale for this forward, or None when inactive."""
+    dp = getattr(module, "drop_path", None)
+    p = getattr(dp, "drop_prob", 0.0) if dp is not None else 0.0
+    if not module.training or p <= 0.0:
+        return None
+    return K.droppath_scale(n_samples, p, mode.seed(getattr(module, "_sm_index", 0), site), device)
 
 
 class _St:
@@ -71,8 +83,9 @@ class MBConv(nn.Module):
 
     def run(self, x, mode):
         c = self.conv
+        dps = droppath_scale(self, x.shape[0], mode, 0, x.device) if self.use_res_connect else None
         st = _St(mode=mode, mid=self.mid, cout=self.out_chans, stride=self.stride, res=self.use_res_connect,
-                 bn0=c[0].bn, bn2=c[2].bn, bn5=c[5].bn)
+                 bn0=c[0].bn, bn2=c[2].bn, bn5=c[5].bn, dp_scale=dps)
         return MBConvFn.apply(x, st, c[0].c.weight, c[0].bn.weight, c[0].bn.bias, c[2].c.weight, c[2].bn.weight,
                               c[2].bn.bias, c[4].fc[0].weight, c[4].fc[2].weight, c[5].c.weight, c[5].bn.weight,
                               c[5].bn.bias)
@@ -136,7 +149,9 @@ class TinyViTBlock(nn.Module):
     def run(self, x, mode):
         Fr, H, Wd, C = x.shape
         st = _St(mode=mode, N=Fr, L=H * Wd, heads=self.num_heads, head_dim=C // self.num_heads,
-                 eps=self.norm1.eps, attn_drop=0.0, seed=0)
+                 eps=self.norm1.eps, attn_drop=0.0, seed_attn=0, drop1=0.0, seed1=0, drop_ff=0.0, seed_ff=0,
+                 drop2=0.0, seed2=0, dp1=droppath_scale(self, Fr, mode, 1, x.device),
+                 dp2=droppath_scale(self, Fr, mode, 2, x.device))
         a, m = self.attn, self.mlp
         y = BlockFn.apply(x.reshape(Fr * H * Wd, C), st, self.norm1.weight, self.norm1.bias, a.qkv.weight,
                           a.qkv.bias, a.proj.weight, a.proj.bias, self.norm2.weight, self.norm2.bias,
@@ -175,10 +190,12 @@ class TinyViT(nn.Module):
                                                window_size=window_sizes[i], drop_path=dpr[cur]))
                 cur += 1
             self.stages.append(_Stage(*blocks))
+        index_modules(self)
 
     # ------------------------------------------------------------------ internals
     def _mode(self):
-        return Mode(torch.is_autocast_enabled("cuda"))
+        from .mae_vit_adapter import next_seed_base
+        return Mode(torch.is_autocast_enabled("cuda"), next_seed_base(self))
 
     def _run_stages(self, x, n_stages, mode):
         for i in range(n_stages):
@@ -213,6 +230,12 @@ class TinyViT(nn.Module):
         t = self.patch_embed.run(x, mode)
         t = self._run_stages(t, 4, mode)
         return t.permute(0, 3, 1, 2)
+
+
+def index_modules(root):
+    """Stable per-module indices for the dropout/DropPath seed derivation."""
+    for i, m in enumerate(root.modules()):
+        m._sm_index = i
 
 
 def tiny_vit_21m_variant(img_size=112, use_checkpoint=True, **kwargs):

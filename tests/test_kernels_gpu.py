@@ -398,3 +398,31 @@ def test_adamw_matches_torch():
     before = p.clone()
     kk.adamw(p, bad, m, v, 5e-4, 0.9, 0.999, 1e-8, 0.05, flag, step)
     assert torch.equal(p, before) and step.item() == 3
+
+
+def test_dropout_masks_fwd_bwd_consistent():
+    """GEMM-epilogue dropout, GELU dropout and their backward kernels regenerate the
+    same counter-hash mask; keep rate ~ 1-p; kept entries scaled by 1/(1-p)."""
+    kk = KK()
+    M, N, Kd, p, seed = 512, 384, 64, 0.1, 1234
+    x = rnd(M, Kd, dtype=torch.bfloat16, seed=1).to(DEV)
+    w = rnd(N, Kd, dtype=torch.bfloat16, seed=2).to(DEV)
+    R = torch.zeros(M, N, dtype=torch.float32, device=DEV)
+    y0 = kk.linear(x, w, out_dtype=torch.float32, residual=R)
+    y = kk.linear(x, w, out_dtype=torch.float32, residual=R, drop_p=p, seed=seed)
+    ratio = (y / y0).cpu()
+    kept = (ratio.abs() > 0.5)
+    assert abs(kept.float().mean().item() - (1 - p)) < 0.01
+    assert torch.allclose(ratio[kept], torch.full_like(ratio[kept], 1 / (1 - p)), rtol=1e-3)
+    g = kk.dropout_bwd(torch.ones(M, N, dtype=torch.float32, device=DEV), p, seed).cpu()
+    assert torch.equal(g > 0, kept)
+    pre = rnd(M, N, dtype=torch.bfloat16, seed=3).to(DEV)
+    h = kk.gelu(pre, p, seed).float().cpu()
+    h0 = kk.gelu(pre).float().cpu()
+    d = kk.gelu_bwd(pre, torch.ones(M, N, dtype=torch.bfloat16, device=DEV), p, seed).float().cpu()
+    km = (h != 0) | (h0 == 0)
+    assert torch.equal((d != 0) | (h0 == 0), km)
+    s = kk.droppath_scale(10000, 0.1, 7, DEV).cpu()
+    vals = torch.unique(s)
+    assert len(vals) == 2 and vals[0] == 0 and abs(vals[1].item() - 1 / 0.9) < 1e-6
+    assert abs((s > 0).float().mean() - 0.9) < 0.02

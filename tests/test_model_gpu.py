@@ -34,9 +34,11 @@ def _build(cfg):
     from ssl_mae_amd.init_rule import apply_rule
     from ssl_mae_amd.mae_vit_adapter import TinyVideoMAE
     from ssl_mae_amd.tiny_vit import tiny_vit_21m_variant
+    from ssl_mae_amd import parity_mode
     enc = tiny_vit_21m_variant(img_size=cfg["dataset"]["image_size"], use_checkpoint=True)
     model = TinyVideoMAE(enc, cfg)
     apply_rule(model)
+    parity_mode(model)
     return model.to(DEV).train()
 
 
@@ -179,7 +181,8 @@ def test_forward_stage3_api_nchw(golden_dir):
     from ssl_mae_amd.tiny_vit import tiny_vit_21m_variant
     d = np.load(os.path.join(golden_dir, "step_b2_t2_s32.npz"))
     B, T, S = int(d["B"]), int(d["T"]), int(d["S"])
-    enc = tiny_vit_21m_variant(img_size=S)
+    from ssl_mae_amd import parity_mode
+    enc = parity_mode(tiny_vit_21m_variant(img_size=S))
     # the golden names are prefixed by 'encoder.'; apply the rule through a wrapper
     wrapper = torch.nn.Module()
     wrapper.encoder = enc
@@ -202,3 +205,40 @@ def test_patchify_unpatchify_roundtrip_and_golden(golden_dir):
     assert np.array_equal(out.cpu().numpy(), d["patchify_out"])
     back = unpatchify(out, *shape[1:], p=8)
     assert torch.equal(back, x)
+
+
+def test_training_regularisers_active_and_replayable():
+    """Dropout (decoder) and DropPath (encoder) are on in train mode: the loss differs
+    from the parity-mode loss, is identical for identical seeds, and a second step
+    draws new masks."""
+    from ssl_mae_amd.init_rule import apply_rule, synthetic_clip
+    from ssl_mae_amd.mae_vit_adapter import TinyVideoMAE
+    from ssl_mae_amd.tiny_vit import tiny_vit_21m_variant
+    from ssl_mae_amd import parity_mode
+    cfg = _cfg(2, 2, 32, 0.75)
+    clip = torch.from_numpy(synthetic_clip(2, 2, 32, seed=3)).to(DEV)
+    mask = torch.zeros(2, 2, 16, dtype=torch.bool, device=DEV)
+    mask[:, :, :12] = True
+
+    def loss_of(parity, seed):
+        torch.manual_seed(seed)
+        m = TinyVideoMAE(tiny_vit_21m_variant(img_size=32), cfg)
+        apply_rule(m)
+        if parity:
+            parity_mode(m)
+        m = m.to(DEV).train()
+        from ssl_mae_amd.functions import mae_loss
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            pred = m(clip, mask)
+        l1 = mae_loss(pred, clip, mask).item()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            pred = m(clip, mask)
+        return l1, mae_loss(pred, clip, mask).item()
+
+    a1, a2 = loss_of(False, 0)
+    b1, b2 = loss_of(False, 0)
+    p1, p2 = loss_of(True, 0)
+    assert a1 == b1 and a2 == b2          # replayable from the seed
+    assert a1 != a2                        # new masks each forward
+    assert p1 == p2                        # parity mode is deterministic
+    assert a1 != p1
