@@ -1,0 +1,85 @@
+"""Kernel micro-benchmarks at the bench shapes (B=256, T=8, 224^2).
+
+python scripts/kbench.py attn [--drop 0.1] [--iters 5]   # decoder (d=64) + encoder (d=32) attention
+python scripts/kbench.py gemm                              # the main GEMM shapes
+Prints per-kernel-group average ms and TFLOP/s measured with HIP events.
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "ssl-vit-video-analytics_amd")]
+
+import torch  # noqa: E402
+
+from ssl_mae_amd import kernels as K  # noqa: E402
+
+
+def timeit(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def attn(args):
+    cases = [("dec d64", args.batch, 6 * 1, 8 * 784, 64, args.drop),
+             ("enc1 d32", args.batch * 8, 6, 3136, 32, 0.0),
+             ("enc2 d32", args.batch * 8, 12, 784, 32, 0.0)]
+    for name, N, H, L, D, p in cases:
+        if args.only and args.only not in name:
+            continue
+        qkv = (torch.randn(N * L, 3 * H * D, device="cuda") * 0.5).to(torch.bfloat16)
+        do = torch.randn(N * L, H * D, device="cuda").to(torch.bfloat16)
+        o, lse = K.attn_fwd(qkv, N, L, H, D, p, 7)
+        f = 4.0 * N * H * L * L * D
+        t_f = timeit(lambda: K.attn_fwd(qkv, N, L, H, D, p, 7), args.iters)
+        t_b = timeit(lambda: K.attn_bwd(qkv, o, do, lse, N, L, H, D, p, 7), args.iters)
+        print(f"{name}: N={N} H={H} L={L} D={D} p={p}  fwd {t_f:8.2f} ms {f / t_f / 1e9:7.1f} TF/s | "
+              f"bwd {t_b:8.2f} ms {3.5 * f / t_b / 1e9:7.1f} TF/s (14 products counted)", flush=True)
+        del qkv, do, o, lse
+        torch.cuda.empty_cache()
+
+
+def gemm(args):
+    B = args.batch
+    cases = [  # (name, M, N, K)
+        ("dec fc1 fwd", B * 6272, 1536, 384), ("dec fc2 fwd", B * 6272, 384, 1536),
+        ("dec qkv fwd", B * 6272, 1152, 384), ("s0 expand fwd", B * 8 * 12544, 384, 96),
+        ("s0 proj fwd", B * 8 * 12544, 96, 384), ("s2 fc1 fwd", B * 8 * 784, 1536, 384)]
+    for name, M, N, Kd in cases:
+        if args.only and args.only not in name:
+            continue
+        x = torch.randn(M, Kd, device="cuda").to(torch.bfloat16)
+        w = torch.randn(N, Kd, device="cuda").to(torch.bfloat16)
+        b = torch.randn(N, device="cuda")
+        f = 2.0 * M * N * Kd
+        t = timeit(lambda: K.linear(x, w, b), args.iters)
+        dy = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+        t_dx = timeit(lambda: K.linear_dx(dy, w), args.iters)
+        sink = torch.zeros(N, Kd, device="cuda")
+        t_dw = timeit(lambda: K.linear_dw(dy, x, sink), args.iters)
+        print(f"{name}: M={M} N={N} K={Kd}  fwd {t:7.2f} ms {f / t / 1e9:7.1f} TF/s | dX {t_dx:7.2f} ms "
+              f"{f / t_dx / 1e9:7.1f} | dW {t_dw:7.2f} ms {f / t_dw / 1e9:7.1f}", flush=True)
+        del x, w, dy, sink
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("what", choices=["attn", "gemm"])
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--drop", type=float, default=0.1)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    from ssl_mae_amd.build import build
+    build()
+    {"attn": attn, "gemm": gemm}[a.what](a)

@@ -58,39 +58,6 @@ SM_DEV int tile_off(int row, int d) {
   (void)CPR;
 }
 
-template <int D>
-SM_DEV bf16x8 row_frag(const char* lds, int row, int s) {
-  const int h = (threadIdx.x & 63) >> 5;
-  return *(const bf16x8*)(lds + tile_off<D>(row, 16 * s + 8 * h));
-}
-
-// A-operand fragment of X^T where X is the [rows][D] tile: lane (r = column d of
-// X, h) element j = X[rb + 16 s + 8 (j>>2) + 4 h + (j&3)][db + r].
-template <int D>
-SM_DEV bf16x8 tr_frag(const char* lds, int rb, int db, int s) {
-  const int l = threadIdx.x & 63;
-  const int h = l >> 5, g1 = (l >> 4) & 1, i = l & 15, q = i >> 2, p = i & 3;
-  const int col = db + 16 * g1 + 4 * p;
-  const int r0 = rb + 16 * s + 4 * h + q;
-  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + tile_off<D>(r0, col)));
-  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + tile_off<D>(r0 + 8, col)));
-  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, v);
-}
-
-// Stage rows [r0, r0+ROWS) of a [L][ld] bf16 matrix (column offset folded into base)
-// into the LDS image; rows >= L are zero.
-template <int D, int ROWS>
-SM_DEV void stage_rows(char* lds, const __bf16* base, int64_t ld, int r0, int L) {
-  constexpr int CHUNKS = ROWS * D / 8;
-  for (int c = threadIdx.x; c < CHUNKS; c += 256) {
-    const int row = c / (D / 8), d = (c % (D / 8)) * 8;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (r0 + row < L) v = *(const uint4*)(base + (int64_t)(r0 + row) * ld + d);
-    *(uint4*)(lds + tile_off<D>(row, d)) = v;
-  }
-}
-
 // accumulator (32x32) -> bf16 B-operand fragment for k-step s
 SM_DEV bf16x8 acc_to_frag(const f32x16& a, int s) {
   bf16x8 f;
@@ -100,34 +67,75 @@ SM_DEV bf16x8 acc_to_frag(const f32x16& a, int s) {
 }
 SM_DEV int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
-// dropout mask on the attention probability P[n,hd,q,k]: row (n*H+hd)*L+q, column k
+// dropout keep multiplier for P[n,hd,q,k] (f32 kernels): row (n*H+hd)*L+q, column k
 SM_DEV float drop_keep_scale(const AttnArgs& a, int n, int hd, int q, int k) {
   const uint64_t row = (uint64_t)(n * a.H + hd) * a.L + q;
   return drop_keep(seed32(a.seed), row, (uint32_t)k, drop_thr(a.drop_p)) ? 1.0f / (1.0f - a.drop_p) : 0.0f;
 }
 
-// Multipliers for the 32 key values a lane holds in a 32x32 accumulator column:
-// keys kb + acc_row(r, h); consecutive keys r, r+1 (r&3 in {0,2}) share one hash.
-SM_DEV void drop_mult_tile(uint32_t rowbase, int kb, int h, int L, uint32_t thr, float ks, float* m) {
+// Per-thread plan for staging a [ROWS][D] bf16 tile (rows of a [L][ld] matrix) into
+// the LDS image: element offsets and LDS offsets are computed once; each tile is
+// then CH 16-byte loads issued early into registers (prefetch) and CH 16-byte
+// LDS stores after the barrier.
+template <int D, int ROWS>
+struct Stager {
+  static constexpr int CH = ROWS * D / 8 / 256;
+  int goff[CH], loff[CH], row[CH];
+  SM_DEV void init(int ld) {
 #pragma unroll
-  for (int r = 0; r < 16; r += 2) {
-    const int key = kb + (r & 3) + 8 * (r >> 2) + 4 * h;
-    const uint32_t hv = drop_hash(rowbase, (uint32_t)key);
-    m[r] = (key < L && drop_keep_bits(hv, (uint32_t)key, thr)) ? ks : 0.f;
-    m[r + 1] = (key + 1 < L && drop_keep_bits(hv, (uint32_t)(key + 1), thr)) ? ks : 0.f;
+    for (int i = 0; i < CH; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      row[i] = c / (D / 8);
+      const int d = (c % (D / 8)) * 8;
+      goff[i] = row[i] * ld + d;
+      loff[i] = tile_off<D>(row[i], d);
+    }
   }
+  SM_DEV void load(const __bf16* base, int rows_left, uint4 (&r)[CH]) const {
+#pragma unroll
+    for (int i = 0; i < CH; ++i)
+      r[i] = row[i] < rows_left ? *(const uint4*)(base + goff[i]) : make_uint4(0, 0, 0, 0);
+  }
+  SM_DEV void store(char* lds, const uint4 (&r)[CH]) const {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) *(uint4*)(lds + loff[i]) = r[i];
+  }
+};
+
+// LDS byte offsets of this lane's fragments (u = 0, s = 0; +32 rows per u and +16
+// rows per s keep the swizzle bits, so those are immediate offsets).
+template <int D>
+SM_DEV int row_frag_off(int s) {   // A/B fragment of 8 consecutive d for row (l & 31)
+  const int l = threadIdx.x & 63;
+  return tile_off<D>(l & 31, 16 * s + 8 * (l >> 5));
+}
+template <int D>
+SM_DEV void tr_frag_off(int t, int& lo, int& hi) {
+  const int l = threadIdx.x & 63;
+  const int h = l >> 5, g1 = (l >> 4) & 1, i = l & 15, q = i >> 2, p = i & 3;
+  const int col = 32 * t + 16 * g1 + 4 * p;
+  lo = tile_off<D>(4 * h + q, col);
+  hi = tile_off<D>(4 * h + q + 8, col);
+}
+SM_DEV bf16x8 lds_b128(const char* lds, int off) { return *(const bf16x8*)(lds + off); }
+SM_DEV bf16x8 lds_tr(const char* lds, int lo, int hi) {
+  s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + lo));
+  s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + hi));
+  s16x8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8, v);
 }
 
 // =============================================================== bf16 forward
 template <int D, bool DROP>
 __global__ __launch_bounds__(256) void attn_fwd_bf16(AttnArgs a) {
   constexpr int KT = 64;
+  constexpr int RB = 32 * D * 2;   // bytes of 32 tile rows
   __shared__ __attribute__((aligned(16))) char lk[KT * D * 2];
   __shared__ __attribute__((aligned(16))) char lv[KT * D * 2];
   const int n = blockIdx.z, hd = blockIdx.y;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5;
   const int C = a.H * D;
-  const int64_t ldq = 3 * (int64_t)C;
+  const int ldq = 3 * C;
   const __bf16* qkv = (const __bf16*)a.qkv + (int64_t)n * a.L * ldq;
   const __bf16* qb = qkv + hd * D;
   const __bf16* kb = qkv + C + hd * D;
@@ -140,6 +148,14 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16(AttnArgs a) {
     if (q < a.L) qf[s] = *(const bf16x8*)(qb + (int64_t)q * ldq + 16 * s + 8 * h);
     else for (int j = 0; j < 8; ++j) qf[s][j] = (__bf16)0.f;
   }
+  Stager<D, KT> stg;
+  stg.init(ldq);
+  int koff[D / 16], vlo[D / 32], vhi[D / 32];
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) koff[s] = row_frag_off<D>(s);
+#pragma unroll
+  for (int t = 0; t < D / 32; ++t) tr_frag_off<D>(t, vlo[t], vhi[t]);
+
   f32x16 o[D / 32];
 #pragma unroll
   for (int t = 0; t < D / 32; ++t)
@@ -149,13 +165,19 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16(AttnArgs a) {
   const float c = a.scale * LOG2E;
   const uint32_t drb = drop_rowbase(seed32(a.seed), (uint64_t)(n * a.H + hd) * a.L + q);
   const uint32_t dthr = drop_thr(a.drop_p);
-  const float dks = DROP ? 1.f / (1.f - a.drop_p) : 1.f;
 
+  uint4 rk[Stager<D, KT>::CH], rv[Stager<D, KT>::CH];
+  stg.load(kb, a.L, rk);
+  stg.load(vb, a.L, rv);
   for (int k0 = 0; k0 < a.L; k0 += KT) {
     __syncthreads();
-    stage_rows<D, KT>(lk, kb, ldq, k0, a.L);
-    stage_rows<D, KT>(lv, vb, ldq, k0, a.L);
+    stg.store(lk, rk);
+    stg.store(lv, rv);
     __syncthreads();
+    if (k0 + KT < a.L) {                       // prefetch the next tile under this tile's math
+      stg.load(kb + (int64_t)(k0 + KT) * ldq, a.L - k0 - KT, rk);
+      stg.load(vb + (int64_t)(k0 + KT) * ldq, a.L - k0 - KT, rv);
+    }
     f32x16 st[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -163,11 +185,9 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16(AttnArgs a) {
       for (int r = 0; r < 16; ++r) st[u][r] = 0.f;
 #pragma unroll
       for (int s = 0; s < D / 16; ++s)
-        st[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(lk, 32 * u + (l & 31), s), qf[s],
-                                                         st[u], 0, 0, 0);
+        st[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_b128(lk, koff[s] + u * RB), qf[s], st[u], 0, 0, 0);
     }
     // raw-score max (scale > 0 keeps the argmax); masking only on the ragged tile
-    float mt = NEG_BIG;
     if (k0 + KT > a.L) {
 #pragma unroll
       for (int u = 0; u < 2; ++u)
@@ -175,6 +195,7 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16(AttnArgs a) {
         for (int r = 0; r < 16; ++r)
           if (k0 + 32 * u + acc_row(r, h) >= a.L) st[u][r] = NEG_BIG;
     }
+    float mt = NEG_BIG;
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -188,14 +209,17 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16(AttnArgs a) {
     float ps = 0.f;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      float dm[16];
-      if (DROP) drop_mult_tile(drb, k0 + 32 * u, h, a.L, dthr, dks, dm);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float p = __builtin_amdgcn_exp2f(fmaf(st[u][r], c, -mn));
-        ps += p;
-        if (DROP) p *= dm[r];
-        st[u][r] = p;
+      for (int g = 0; g < 4; ++g) {
+        uint32_t hv = 0;
+        if (DROP) hv = drop_hash(drb, (uint32_t)(k0 + 32 * u + 8 * g + 4 * h));   // keys 4g'..+3 share it
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = 4 * g + j;
+          const float p = __builtin_amdgcn_exp2f(fmaf(st[u][r], c, -mn));
+          ps += p;
+          st[u][r] = (!DROP || ((hv >> (8 * j)) & 0xFFu) >= dthr) ? p : 0.f;
+        }
       }
     }
     lsum = lsum * alpha + ps;
@@ -212,12 +236,13 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16(AttnArgs a) {
         const bf16x8 pf = acc_to_frag(st[u], s);
 #pragma unroll
         for (int t = 0; t < D / 32; ++t)
-          o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(lv, 32 * u, 32 * t, s), pf, o[t], 0, 0, 0);
+          o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              lds_tr(lv, vlo[t] + u * RB + s * (RB / 2), vhi[t] + u * RB + s * (RB / 2)), pf, o[t], 0, 0, 0);
       }
   }
   lsum += __shfl_xor(lsum, 32, 64);
   if (q < a.L) {
-    const float inv = 1.f / lsum;
+    const float inv = (DROP ? 1.f / (1.f - a.drop_p) : 1.f) / lsum;
     __bf16* ob = (__bf16*)a.out + ((int64_t)n * a.L + q) * C + hd * D;
 #pragma unroll
     for (int t = 0; t < D / 32; ++t)
@@ -252,9 +277,12 @@ __global__ void attn_delta_kernel(AttnArgs a, int D) {
 }
 
 // =============================================================== bf16 backward dK, dV
+// Keys on lanes (32 per wave, 128 per block); Q / dO tiles (64 rows) staged to LDS
+// with register prefetch and read both row-wise (S, dP) and transposed (dV, dK).
 template <int D, bool DROP>
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(AttnArgs a) {
   constexpr int QT = 64;
+  constexpr int RB = 32 * D * 2;
   __shared__ __attribute__((aligned(16))) char lq[QT * D * 2];
   __shared__ __attribute__((aligned(16))) char ldo[QT * D * 2];
   __shared__ __attribute__((aligned(16))) float llse[QT];
@@ -262,7 +290,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(AttnArgs a) {
   const int n = blockIdx.z, hd = blockIdx.y;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5;
   const int C = a.H * D;
-  const int64_t ldq = 3 * (int64_t)C;
+  const int ldq = 3 * C;
   const __bf16* qkv = (const __bf16*)a.qkv + (int64_t)n * a.L * ldq;
   const __bf16* qb = qkv + hd * D;
   const __bf16* kb = qkv + C + hd * D;
@@ -282,23 +310,43 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(AttnArgs a) {
       for (int j = 0; j < 8; ++j) { kf[s][j] = (__bf16)0.f; vf[s][j] = (__bf16)0.f; }
     }
   }
+  Stager<D, QT> sq, sd;
+  sq.init(ldq);
+  sd.init(C);
+  int roff[D / 16], tlo[D / 32], thi[D / 32];
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) roff[s] = row_frag_off<D>(s);
+#pragma unroll
+  for (int t = 0; t < D / 32; ++t) tr_frag_off<D>(t, tlo[t], thi[t]);
+
   f32x16 dk[D / 32], dv[D / 32];
 #pragma unroll
   for (int t = 0; t < D / 32; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) { dk[t][r] = 0.f; dv[t][r] = 0.f; }
   const float c = a.scale * LOG2E;
+  const float ks = DROP ? 1.f / (1.f - a.drop_p) : 1.f;
+  const uint32_t s32 = seed32(a.seed), dthr = drop_thr(a.drop_p);
+  const int kq = l & 3;                       // == key & 3: byte of the shared hash
+  const uint64_t row0 = (uint64_t)(n * a.H + hd) * a.L;
 
+  uint4 rq[Stager<D, QT>::CH], rd[Stager<D, QT>::CH];
+  sq.load(qb, a.L, rq);
+  sd.load(dob, a.L, rd);
   for (int q0 = 0; q0 < a.L; q0 += QT) {
     __syncthreads();
-    stage_rows<D, QT>(lq, qb, ldq, q0, a.L);
-    stage_rows<D, QT>(ldo, dob, C, q0, a.L);
+    sq.store(lq, rq);
+    sd.store(ldo, rd);
     if (threadIdx.x < QT) {
       const int qq = q0 + threadIdx.x;
       llse[threadIdx.x] = qq < a.L ? lse[qq] * LOG2E : 1e30f;   // invalid rows -> P = 0
       ldel[threadIdx.x] = qq < a.L ? del[qq] : 0.f;
     }
     __syncthreads();
+    if (q0 + QT < a.L) {
+      sq.load(qb + (int64_t)(q0 + QT) * ldq, a.L - q0 - QT, rq);
+      sd.load(dob + (int64_t)(q0 + QT) * C, a.L - q0 - QT, rd);
+    }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       f32x16 sacc, dpacc;
@@ -306,11 +354,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(AttnArgs a) {
       for (int r = 0; r < 16; ++r) { sacc[r] = 0.f; dpacc[r] = 0.f; }
 #pragma unroll
       for (int s = 0; s < D / 16; ++s) {
-        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(lq, 32 * u + (l & 31), s), kf[s], sacc, 0, 0, 0);
-        dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(ldo, 32 * u + (l & 31), s), vf[s], dpacc, 0, 0, 0);
+        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_b128(lq, roff[s] + u * RB), kf[s], sacc, 0, 0, 0);
+        dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_b128(ldo, roff[s] + u * RB), vf[s], dpacc, 0, 0, 0);
       }
-      // rows = queries (regs), column = this lane's key.  Row constants come in
-      // as 16-B LDS reads (4 consecutive query rows per register group).
       float lse4[16], del4[16];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -319,24 +365,22 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(AttnArgs a) {
         lse4[4 * g] = a4.x; lse4[4 * g + 1] = a4.y; lse4[4 * g + 2] = a4.z; lse4[4 * g + 3] = a4.w;
         del4[4 * g] = b4.x; del4[4 * g + 1] = b4.y; del4[4 * g + 2] = b4.z; del4[4 * g + 3] = b4.w;
       }
-      float dmul[16];
+      uint32_t hsh[16];
       if (DROP) {
-        // keys 2j, 2j+1 (lanes l, l^1) share one hash per query row: each lane
-        // hashes every other row and swaps with its partner through DPP.
-        const uint32_t thr = drop_thr(a.drop_p);
-        const float ks = 1.f / (1.f - a.drop_p);
-        const bool odd = key & 1;
-        const uint32_t s32 = seed32(a.seed);
-        const uint64_t rbase = (uint64_t)(n * a.H + hd) * a.L + q0 + 32 * u;
+        // one hash per (query row, 4-key group): the quad's lanes (keys 4m..4m+3)
+        // each hash the rows r = 4g + lane&3, then broadcast within the quad (DPP)
+        uint32_t mine[4];
 #pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-          const int qi = acc_row(r + (odd ? 1 : 0), h);
-          const uint32_t mine = drop_hash(drop_rowbase(s32, rbase + qi), (uint32_t)key);
-          const uint32_t other = (uint32_t)__builtin_amdgcn_mov_dpp((int)mine, 0xB1, 0xF, 0xF, false);
-          const uint32_t h0 = odd ? other : mine, h1 = odd ? mine : other;   // rows r, r+1
-          const bool v0 = q0 + 32 * u + acc_row(r, h) < a.L, v1 = q0 + 32 * u + acc_row(r + 1, h) < a.L;
-          dmul[r] = (v0 && drop_keep_bits(h0, (uint32_t)key, thr)) ? ks : 0.f;
-          dmul[r + 1] = (v1 && drop_keep_bits(h1, (uint32_t)key, thr)) ? ks : 0.f;
+        for (int g = 0; g < 4; ++g) {
+          const int qr = q0 + 32 * u + 8 * g + 4 * h + kq;        // acc_row(4g + kq, h)
+          mine[g] = drop_hash(drop_rowbase(s32, row0 + qr), (uint32_t)key);
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          hsh[4 * g + 0] = (uint32_t)__builtin_amdgcn_mov_dpp((int)mine[g], 0x00, 0xF, 0xF, false);
+          hsh[4 * g + 1] = (uint32_t)__builtin_amdgcn_mov_dpp((int)mine[g], 0x55, 0xF, 0xF, false);
+          hsh[4 * g + 2] = (uint32_t)__builtin_amdgcn_mov_dpp((int)mine[g], 0xAA, 0xF, 0xF, false);
+          hsh[4 * g + 3] = (uint32_t)__builtin_amdgcn_mov_dpp((int)mine[g], 0xFF, 0xF, 0xF, false);
         }
       }
 #pragma unroll
@@ -344,12 +388,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(AttnArgs a) {
         const float p = __builtin_amdgcn_exp2f(fmaf(sacc[r], c, -lse4[r]));
         float dp = dpacc[r];
         if (DROP) {
-          dp *= dmul[r];
-          sacc[r] = p * dmul[r];         // dropped P feeds dV
+          const bool keep = ((hsh[r] >> (8 * kq)) & 0xFFu) >= dthr;
+          dp = keep ? dp * ks : 0.f;
+          sacc[r] = keep ? p * ks : 0.f;   // dropped P feeds dV
         } else {
           sacc[r] = p;
         }
-        dpacc[r] = p * (dp - del4[r]);   // dS
+        dpacc[r] = p * (dp - del4[r]);     // dS
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -357,8 +402,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(AttnArgs a) {
         const bf16x8 sf = acc_to_frag(dpacc, s);
 #pragma unroll
         for (int t = 0; t < D / 32; ++t) {
-          dv[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(ldo, 32 * u, 32 * t, s), pf, dv[t], 0, 0, 0);
-          dk[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(lq, 32 * u, 32 * t, s), sf, dk[t], 0, 0, 0);
+          const int ob = u * RB + s * (RB / 2);
+          dv[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr(ldo, tlo[t] + ob, thi[t] + ob), pf, dv[t], 0, 0, 0);
+          dk[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr(lq, tlo[t] + ob, thi[t] + ob), sf, dk[t], 0, 0, 0);
         }
       }
     }
@@ -379,15 +425,17 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(AttnArgs a) {
 }
 
 // =============================================================== bf16 backward dQ
+// Queries on lanes; K / V tiles staged with prefetch; dQ^T = K^T dS^T.
 template <int D, bool DROP>
 __global__ __launch_bounds__(256) void attn_bwd_dq_bf16(AttnArgs a) {
   constexpr int KT = 64;
+  constexpr int RB = 32 * D * 2;
   __shared__ __attribute__((aligned(16))) char lk[KT * D * 2];
   __shared__ __attribute__((aligned(16))) char lv[KT * D * 2];
   const int n = blockIdx.z, hd = blockIdx.y;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5;
   const int C = a.H * D;
-  const int64_t ldq = 3 * (int64_t)C;
+  const int ldq = 3 * C;
   const __bf16* qkv = (const __bf16*)a.qkv + (int64_t)n * a.L * ldq;
   const __bf16* qb = qkv + hd * D;
   const __bf16* kb = qkv + C + hd * D;
@@ -408,21 +456,36 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_bf16(AttnArgs a) {
       for (int j = 0; j < 8; ++j) { qf[s][j] = (__bf16)0.f; df[s][j] = (__bf16)0.f; }
     }
   }
+  Stager<D, KT> stg;
+  stg.init(ldq);
+  int roff[D / 16], tlo[D / 32], thi[D / 32];
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) roff[s] = row_frag_off<D>(s);
+#pragma unroll
+  for (int t = 0; t < D / 32; ++t) tr_frag_off<D>(t, tlo[t], thi[t]);
   f32x16 dq[D / 32];
 #pragma unroll
   for (int t = 0; t < D / 32; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) dq[t][r] = 0.f;
   const float c = a.scale * LOG2E;
+  const float ks = DROP ? 1.f / (1.f - a.drop_p) : 1.f;
   const uint32_t drb = drop_rowbase(seed32(a.seed), (uint64_t)(n * a.H + hd) * a.L + q);
   const uint32_t dthr = drop_thr(a.drop_p);
-  const float dks = DROP ? 1.f / (1.f - a.drop_p) : 1.f;
 
+  uint4 rk[Stager<D, KT>::CH], rv[Stager<D, KT>::CH];
+  stg.load(kb, a.L, rk);
+  stg.load(vb, a.L, rv);
   for (int k0 = 0; k0 < a.L; k0 += KT) {
     __syncthreads();
-    stage_rows<D, KT>(lk, kb, ldq, k0, a.L);
-    stage_rows<D, KT>(lv, vb, ldq, k0, a.L);
+    stg.store(lk, rk);
+    stg.store(lv, rv);
     __syncthreads();
+    if (k0 + KT < a.L) {
+      stg.load(kb + (int64_t)(k0 + KT) * ldq, a.L - k0 - KT, rk);
+      stg.load(vb + (int64_t)(k0 + KT) * ldq, a.L - k0 - KT, rv);
+    }
+    const bool ragged = k0 + KT > a.L;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       f32x16 sacc, dpacc;
@@ -430,25 +493,31 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_bf16(AttnArgs a) {
       for (int r = 0; r < 16; ++r) { sacc[r] = 0.f; dpacc[r] = 0.f; }
 #pragma unroll
       for (int s = 0; s < D / 16; ++s) {
-        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(lk, 32 * u + (l & 31), s), qf[s], sacc, 0, 0, 0);
-        dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(lv, 32 * u + (l & 31), s), df[s], dpacc, 0, 0, 0);
+        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_b128(lk, roff[s] + u * RB), qf[s], sacc, 0, 0, 0);
+        dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_b128(lv, roff[s] + u * RB), df[s], dpacc, 0, 0, 0);
       }
-      float dm[16];
-      if (DROP) drop_mult_tile(drb, k0 + 32 * u, h, a.L, dthr, dks, dm);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = k0 + 32 * u + acc_row(r, h);
-        float p = key < a.L ? __builtin_amdgcn_exp2f(fmaf(sacc[r], c, -lse2)) : 0.f;
-        float dp = dpacc[r];
-        if (DROP) dp *= dm[r];
-        dpacc[r] = p * (dp - dl);
+      for (int g = 0; g < 4; ++g) {
+        uint32_t hv = 0;
+        if (DROP) hv = drop_hash(drb, (uint32_t)(k0 + 32 * u + 8 * g + 4 * h));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = 4 * g + j;
+          float p = __builtin_amdgcn_exp2f(fmaf(sacc[r], c, -lse2));
+          if (ragged && k0 + 32 * u + acc_row(r, h) >= a.L) p = 0.f;
+          float dp = dpacc[r];
+          if (DROP) dp = ((hv >> (8 * j)) & 0xFFu) >= dthr ? dp * ks : 0.f;
+          dpacc[r] = p * (dp - dl);
+        }
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const bf16x8 sf = acc_to_frag(dpacc, s);
 #pragma unroll
-        for (int t = 0; t < D / 32; ++t)
-          dq[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(lk, 32 * u, 32 * t, s), sf, dq[t], 0, 0, 0);
+        for (int t = 0; t < D / 32; ++t) {
+          const int ob = u * RB + s * (RB / 2);
+          dq[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr(lk, tlo[t] + ob, thi[t] + ob), sf, dq[t], 0, 0, 0);
+        }
       }
     }
   }

@@ -99,12 +99,14 @@ SM_DEV float block_sum(float v, float* red) {
 
 // ---------------------------------------------------------------- counter RNG
 // Dropout / DropPath masks are a pure function of (seed, row, column):
-//   h    = fmix32(seed32 + row * 0x9E3779B1 + (col >> 1) * 0x7FEB352D)
-//   bits = (col & 1) ? h >> 16 : h & 0xFFFF          (one hash per column pair)
-//   keep = bits >= round(p * 65536), kept values scaled by 1/(1-p)
-// so every kernel that touches an element (forward, checkpoint recompute,
-// backward) regenerates the same mask without storing it.  `row` is the tensor
-// row (or the attention row (n*H + h)*L + q); fmix32 is MurmurHash3's finalizer.
+//   h    = fmix32(seed32 + row * 0x9E3779B1 + (col >> 2) * 0x7FEB352D)
+//   byte = (h >> 8 * (col & 3)) & 0xFF                 (one hash per 4 columns)
+//   keep = byte >= round(256 p)                        (kept values scaled by 1/(1-p))
+// Every kernel that touches an element (forward, checkpoint recompute, backward)
+// regenerates the same mask without storing it.  `row` is the tensor row (or the
+// attention row (n*H + h)*L + q); fmix32 is MurmurHash3's finalizer.  The 8-bit
+// keep threshold is the FlashAttention-2 convention (what the reference's GPU
+// SDPA uses): for p = 0.1 the drop rate is 26/256.
 SM_DEV uint32_t fmix32(uint32_t h) {
   h ^= h >> 16;
   h *= 0x85EBCA6Bu;
@@ -115,10 +117,10 @@ SM_DEV uint32_t fmix32(uint32_t h) {
 }
 SM_DEV uint32_t seed32(uint64_t seed) { return (uint32_t)seed ^ (uint32_t)(seed >> 32); }
 SM_DEV uint32_t drop_rowbase(uint32_t s32, uint64_t row) { return s32 + (uint32_t)row * 0x9E3779B1u; }
-SM_DEV uint32_t drop_hash(uint32_t rowbase, uint32_t col) { return fmix32(rowbase + (col >> 1) * 0x7FEB352Du); }
-SM_DEV uint32_t drop_thr(float p) { return (uint32_t)(p * 65536.f + 0.5f); }
+SM_DEV uint32_t drop_hash(uint32_t rowbase, uint32_t col) { return fmix32(rowbase + (col >> 2) * 0x7FEB352Du); }
+SM_DEV uint32_t drop_thr(float p) { return (uint32_t)(p * 256.f + 0.5f); }
 SM_DEV bool drop_keep_bits(uint32_t h, uint32_t col, uint32_t thr) {
-  return ((col & 1) ? (h >> 16) : (h & 0xFFFFu)) >= thr;
+  return ((h >> ((col & 3) * 8)) & 0xFFu) >= thr;
 }
 SM_DEV bool drop_keep(uint32_t s32, uint64_t row, uint32_t col, uint32_t thr) {
   return drop_keep_bits(drop_hash(drop_rowbase(s32, row), col), col, thr);

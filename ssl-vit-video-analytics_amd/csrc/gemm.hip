@@ -241,10 +241,10 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
           const uint32_t rb = drop_rowbase(seed32(g.seed), (uint64_t)row), thr = drop_thr(g.drop_p);
           const float ks = 1.f / (1.f - g.drop_p);
 #pragma unroll
-          for (int e = 0; e < 8; e += 2) {
-            const uint32_t hv = drop_hash(rb, (uint32_t)(col0 + e));
-            v[e] *= drop_keep_bits(hv, (uint32_t)(col0 + e), thr) ? ks : 0.f;
-            v[e + 1] *= drop_keep_bits(hv, (uint32_t)(col0 + e + 1), thr) ? ks : 0.f;
+          for (int e4 = 0; e4 < 8; e4 += 4) {
+            const uint32_t hv = drop_hash(rb, (uint32_t)(col0 + e4));   // col0 % 8 == 0
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e4 + e] *= ((hv >> (8 * e)) & 0xFFu) >= thr ? ks : 0.f;
           }
         }
         if (g.row_scale) {

@@ -145,6 +145,46 @@ def test_attention_dropout_statistics():
     assert rel_err(mean, o0.float()) < 0.1
 
 
+def _np_keep(rows, cols, p, seed):
+    """numpy restatement of csrc/common.h drop_keep (counter hash, 8-bit threshold,
+    one fmix32 per 4 columns): keep[row, col] for the given index vectors."""
+    M = 0xFFFFFFFF
+    s32 = (seed & M) ^ (seed >> 32)
+    r = rows.astype(np.uint64)[:, None]
+    c = cols.astype(np.uint64)[None, :]
+    h = (s32 + r * 0x9E3779B1 + (c >> 2) * 0x7FEB352D) & M
+    h ^= h >> 16; h = (h * 0x85EBCA6B) & M
+    h ^= h >> 13; h = (h * 0xC2B2AE35) & M
+    h ^= h >> 16
+    byte = (h >> ((c & 3) * 8)) & 0xFF
+    return byte >= int(p * 256 + 0.5)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("D,L", [(64, 200), (32, 130)])
+def test_attention_dropout_exact_mask(dtype, D, L):
+    """Attention with dropout equals an fp32 torch reference that applies the
+    counter-hash mask regenerated on the host -- forward and all three gradients
+    (checks the fwd, dK/dV and dQ kernels regenerate the identical mask)."""
+    N, H, p, seed = 2, 3, 0.1, 987654321
+    qkv = rnd(N * L, 3 * H * D, dtype=dtype, seed=60 + L)
+    dO = rnd(N * L, H * D, dtype=dtype, seed=61 + L)
+    q, k, v = [t.detach().clone().requires_grad_(True)
+               for t in qkv.float().reshape(N, L, 3, H, D).permute(2, 0, 3, 1, 4)]
+    rows = np.arange(N * H * L)
+    keep = torch.from_numpy(_np_keep(rows, np.arange(L), p, seed)).reshape(N, H, L, L)
+    P = torch.softmax((q @ k.transpose(-1, -2)) / math.sqrt(D), -1)
+    o_ref = (P * keep / (1 - p)) @ v
+    o_ref_flat = o_ref.transpose(1, 2).reshape(N * L, H * D)
+    o_ref_flat.backward(dO.float())
+    dqkv_ref = torch.stack([q.grad, k.grad, v.grad]).permute(1, 3, 0, 2, 4).reshape(N * L, 3 * H * D)
+    kk = KK()
+    o, lse = kk.attn_fwd(qkv.to(DEV), N, L, H, D, drop_p=p, seed=seed)
+    assert rel_err(o, o_ref_flat) < TOL[dtype]
+    dqkv = kk.attn_bwd(qkv.to(DEV), o, dO.to(DEV), lse, N, L, H, D, p, seed)
+    assert rel_err(dqkv, dqkv_ref) < (1e-4 if dtype == torch.float32 else 3e-2)
+
+
 # ------------------------------------------------------------------ LayerNorm
 @pytest.mark.parametrize("xd,yd", [(torch.float32, torch.float32), (torch.bfloat16, torch.bfloat16),
                                    (torch.float32, torch.bfloat16)])
