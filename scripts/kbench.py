@@ -72,9 +72,26 @@ def gemm(args):
         torch.cuda.empty_cache()
 
 
+def gemmk(args):
+    """Fixed-cost probe: one output shape, growing K (fwd layout, bf16 out, bias)."""
+    M, N = args.batch * 6272, 1152
+    for Kd in (64, 128, 256, 384, 768, 1536):
+        x = torch.randn(M, Kd, device="cuda").to(torch.bfloat16)
+        w = torch.randn(N, Kd, device="cuda").to(torch.bfloat16)
+        b = torch.randn(N, device="cuda")
+        f = 2.0 * M * N * Kd
+        t = timeit(lambda: K.linear(x, w, b), args.iters)
+        t0 = timeit(lambda: K.linear(x, w), args.iters)
+        gb = (M * Kd + M * N) * 2 / 1e9
+        print(f"M={M} N={N} K={Kd}: {t:7.3f} ms {f / t / 1e9:7.1f} TF/s {gb / t:7.1f} TB/s | no-bias {t0:7.3f} ms",
+              flush=True)
+        del x, w
+        torch.cuda.empty_cache()
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["attn", "gemm"])
+    ap.add_argument("what", choices=["attn", "gemm", "gemmk"])
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--drop", type=float, default=0.1)
     ap.add_argument("--iters", type=int, default=5)
@@ -82,4 +99,4 @@ if __name__ == "__main__":
     a = ap.parse_args()
     from ssl_mae_amd.build import build
     build()
-    {"attn": attn, "gemm": gemm}[a.what](a)
+    {"attn": attn, "gemm": gemm, "gemmk": gemmk}[a.what](a)

@@ -127,13 +127,157 @@ SM_DEV bf16x8 lread_frag(const char* lds, int rb, int s) {
   }
 }
 
-template <bool AK, bool BK, typename TC>
+// Epilogue of one 128x128 tile from the (swapped-operand) accumulators.
+template <typename TC, bool VEC>
+SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[2][2], int m0, int n0,
+                                                         int wm, int wn, int l) {
+  // The MFMAs run with swapped operands (D = B_frag x A_frag), so each lane owns
+  // one output ROW (token) and registers r hold its columns
+  // wn + 32j + (r&3) + 8(r>>2) + 4h: row-per-lane, no LDS round trip.
+  const int h = l >> 5;
+  const int64_t rbase = m0 + wm + (l & 31);
+  if (!VEC) {   // N % 8 or ldc % 8 != 0 (launch-uniform; chosen at launch)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t row = rbase + 32 * i;
+      if (row >= g.M) continue;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int col = n0 + wn + 32 * j + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (col < g.N) epilogue_store<TC>(g, row, col, acc[i][j][r]);
+        }
+    }
+    return;
+  }
+  // Row-run epilogue: one v_permlane32_swap per register pair gives every lane two
+  // runs of 8 consecutive columns per (i, j): cols wn + 32j + 16p + 8h + 0..7,
+  // values acc[i][j][8p + 0..3] and acc[i][j][8p + 4..7].  All epilogue math is
+  // per element on those runs; each run is one 16-B (bf16) / 32-B (fp32) store.
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[i][j][8 * p + e]),
+                                                     __float_as_uint(acc[i][j][8 * p + 4 + e]), false, false);
+          acc[i][j][8 * p + e] = __uint_as_float(sw[0]);
+          acc[i][j][8 * p + 4 + e] = __uint_as_float(sw[1]);
+        }
+  if (g.partial) {   // split-K: raw fp32 runs into this z's slab
+    float* slab = g.partial + (int64_t)blockIdx.z * g.M * g.N;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t row = rbase + 32 * i;
+      if (row >= g.M) continue;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const int col = n0 + wn + 32 * j + 16 * p + 8 * h;
+          if (col < g.N) {
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = acc[i][j][8 * p + e];
+            store8(slab + row * g.N + col, v);
+          }
+        }
+    }
+    return;
+  }
+  const bool bias_vec = g.bias && ((uintptr_t)g.bias & 15) == 0;
+  const bool has_r = g.beta != 0.f;
+  const TC* Rsrc = g.R ? (const TC*)g.R : (const TC*)g.C;
+  const uint32_t s32 = seed32(g.seed), thr = drop_thr(g.drop_p);
+  const float ks = g.drop_p > 0.f ? 1.f / (1.f - g.drop_p) : 1.f;
+  constexpr int RW = sizeof(TC) * 8 / 16;   // 16-B words per 8-column run
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int64_t row = rbase + 32 * i;
+    if (row >= g.M) continue;
+    const float rs = g.row_scale ? g.row_scale[row / g.rows_per_group] : 1.f;
+    const uint32_t rb = drop_rowbase(s32, (uint64_t)row);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      uint4 rr[2][RW];   // the residual runs of this (row, j), in flight before the stores (R may alias C)
+      if (has_r) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const int col = n0 + wn + 32 * j + 16 * p + 8 * h;
+          if (col < g.N) {
+            const uint4* src = (const uint4*)(Rsrc + row * g.ldc + col);
+#pragma unroll
+            for (int q = 0; q < RW; ++q) rr[p][q] = src[q];
+          }
+        }
+      }
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int col = n0 + wn + 32 * j + 16 * p + 8 * h;
+        if (col >= g.N) continue;
+        float b8[8];
+        if (bias_vec) {
+          const float4 b0 = *(const float4*)(g.bias + col);
+          const float4 b1 = *(const float4*)(g.bias + col + 4);
+          b8[0] = b0.x; b8[1] = b0.y; b8[2] = b0.z; b8[3] = b0.w; b8[4] = b1.x; b8[5] = b1.y; b8[6] = b1.z; b8[7] = b1.w;
+        } else if (g.bias) {   // a flat-buffer parameter view need not be 16-B aligned
+#pragma unroll
+          for (int e = 0; e < 8; ++e) b8[e] = g.bias[col + e];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) b8[e] = 0.f;
+        }
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          v[e] = fmaf(acc[i][j][8 * p + e], g.alpha, b8[e]);
+          if (g.epi & 2) v[e] = (float)(__bf16)v[e];
+        }
+        const int64_t idx = row * g.ldc + col;
+        if (g.epi & 1) {
+          if (g.aux) store8((TC*)g.aux + idx, v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = gelu_f(v[e]);
+        }
+        if (g.drop_p > 0.f) {
+#pragma unroll
+          for (int e4 = 0; e4 < 8; e4 += 4) {
+            const uint32_t hv = drop_hash(rb, (uint32_t)(col + e4));   // col % 8 == 0
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e4 + e] *= ((hv >> (8 * e)) & 0xFFu) >= thr ? ks : 0.f;
+          }
+        }
+        if (g.row_scale) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] *= rs;
+        }
+        if (has_r) {
+          float r8[8];
+          load8((const TC*)&rr[p][0], r8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = fmaf(g.beta, r8[e], v[e]);
+        }
+        store8((TC*)g.C + idx, v);
+      }
+    }
+  }
+}
+
+// One 128x128 output tile per block; 1-D grid over (m-tile, n-tile) with an
+// XCD-aware bijective remap: the n-tiles of one m-tile (which share the A panel)
+// are dispatched to the same XCD's L2.  (A persistent variant that prefetched the
+// next tile's first K-step under the epilogue measured 5-20 % slower: with three
+// resident blocks per CU the hardware already overlaps one block's epilogue with
+// another's prologue.)
+template <bool AK, bool BK, typename TC, bool VEC>
 __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) char lds[2 * BM * BKT * 2];
   char* la = lds;
   char* lb = lds + BM * BKT * 2;
-  // 1-D grid over (m-tile, n-tile) with an XCD-aware bijective remap: the n-tiles
-  // of one m-tile (which share the A panel) are dispatched to the same XCD's L2.
   const int ntn = (g.N + BN - 1) / BN;
   const int nwg = gridDim.x;
   const int bid = blockIdx.x;
@@ -179,90 +323,11 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
     __syncthreads();
   }
-  const int h = l >> 5;
-  if (g.partial || (g.N & 7) || (g.ldc & 7)) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int col = n0 + wn + 32 * j + (l & 31);
-        if (col >= g.N) continue;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int64_t row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
-          if (row < g.M) epilogue_store<TC>(g, row, col, acc[i][j][r]);
-        }
-      }
-    return;
-  }
-  // Row-vector epilogue: the fp32 accumulators are staged through LDS (half the
-  // tile at a time: rows {32i..32i+31} of each wave row-group), then every thread
-  // finishes 8 consecutive columns of a row: bias, GELU (+aux), dropout (one hash
-  // per column pair), DropPath row scale, residual — all as 16-byte vectors.
-  float* stg = (float*)lds;  // [64][128] fp32 = 32 KB (the operand tiles are dead)
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int srow = (w >> 1) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        stg[srow * 128 + wn + 32 * j + (l & 31)] = acc[i][j][r];
-      }
-    __syncthreads();
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int cidx = threadIdx.x + 256 * it;      // 64 rows x 16 chunks
-      const int srow = cidx >> 4, cc = (cidx & 15) * 8;
-      const int64_t row = m0 + (srow >> 5) * 64 + 32 * i + (srow & 31);
-      const int col0 = n0 + cc;
-      if (row < g.M && col0 < g.N) {
-        float v[8];
-        const float4 a0 = *(const float4*)(stg + srow * 128 + cc);
-        const float4 a1 = *(const float4*)(stg + srow * 128 + cc + 4);
-        v[0] = a0.x; v[1] = a0.y; v[2] = a0.z; v[3] = a0.w; v[4] = a1.x; v[5] = a1.y; v[6] = a1.z; v[7] = a1.w;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          v[e] *= g.alpha;
-          if (g.bias) v[e] += g.bias[col0 + e];
-          if (g.epi & 2) v[e] = (float)(__bf16)v[e];
-        }
-        const int64_t idx = row * g.ldc + col0;
-        if (g.epi & 1) {
-          if (g.aux) store8((TC*)g.aux + idx, v);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = gelu_f(v[e]);
-        }
-        if (g.drop_p > 0.f) {
-          const uint32_t rb = drop_rowbase(seed32(g.seed), (uint64_t)row), thr = drop_thr(g.drop_p);
-          const float ks = 1.f / (1.f - g.drop_p);
-#pragma unroll
-          for (int e4 = 0; e4 < 8; e4 += 4) {
-            const uint32_t hv = drop_hash(rb, (uint32_t)(col0 + e4));   // col0 % 8 == 0
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e4 + e] *= ((hv >> (8 * e)) & 0xFFu) >= thr ? ks : 0.f;
-          }
-        }
-        if (g.row_scale) {
-          const float rs = g.row_scale[row / g.rows_per_group];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] *= rs;
-        }
-        if (g.beta != 0.f) {
-          float rr[8];
-          load8(g.R ? (const TC*)g.R + idx : (const TC*)g.C + idx, rr);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += g.beta * rr[e];
-        }
-        store8((TC*)g.C + idx, v);
-      }
-    }
-    __syncthreads();
-  }
+  gemm_epilogue<TC, VEC>(g, acc, m0, n0, wm, wn, l);
 }
 
 // ============================================================ f32 MFMA kernel
@@ -359,8 +424,14 @@ template <bool AK, bool BK>
 int launch_layout(int abt, int ct, GemmArgs g, int splits, hipStream_t st) {
   if (abt == SM_BF16) {
     dim3 grid(((g.N + BN - 1) / BN) * ((g.M + BM - 1) / BM), 1, splits);
-    if (ct == SM_BF16) hipLaunchKernelGGL((gemm_bf16_kernel<AK, BK, __bf16>), grid, dim3(256), 0, st, g);
-    else hipLaunchKernelGGL((gemm_bf16_kernel<AK, BK, float>), grid, dim3(256), 0, st, g);
+    const bool vec = !((g.N & 7) || (!g.partial && (g.ldc & 7)));
+    if (ct == SM_BF16) {
+      if (vec) hipLaunchKernelGGL((gemm_bf16_kernel<AK, BK, __bf16, true>), grid, dim3(256), 0, st, g);
+      else hipLaunchKernelGGL((gemm_bf16_kernel<AK, BK, __bf16, false>), grid, dim3(256), 0, st, g);
+    } else {
+      if (vec) hipLaunchKernelGGL((gemm_bf16_kernel<AK, BK, float, true>), grid, dim3(256), 0, st, g);
+      else hipLaunchKernelGGL((gemm_bf16_kernel<AK, BK, float, false>), grid, dim3(256), 0, st, g);
+    }
   } else {
     if (ct != SM_F32) return -3;
     dim3 grid(((g.N + FBN - 1) / FBN) * ((g.M + FBM - 1) / FBM), 1, splits);
