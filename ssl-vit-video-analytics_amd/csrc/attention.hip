@@ -127,7 +127,7 @@ SM_DEV bf16x8 lds_tr(const char* lds, int lo, int hi) {
 
 // =============================================================== bf16 forward
 template <int D, bool DROP>
-__global__ __launch_bounds__(256) void attn_fwd_bf16(AttnArgs a) {
+__global__ __launch_bounds__(256, 2) void attn_fwd_bf16(AttnArgs a) {
   constexpr int KT = 64;
   constexpr int RB = 32 * D * 2;   // bytes of 32 tile rows
   __shared__ __attribute__((aligned(16))) char lk[KT * D * 2];
@@ -280,7 +280,7 @@ __global__ void attn_delta_kernel(AttnArgs a, int D) {
 // Keys on lanes (32 per wave, 128 per block); Q / dO tiles (64 rows) staged to LDS
 // with register prefetch and read both row-wise (S, dP) and transposed (dV, dK).
 template <int D, bool DROP>
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(AttnArgs a) {
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(AttnArgs a) {
   constexpr int QT = 64;
   constexpr int RB = 32 * D * 2;
   __shared__ __attribute__((aligned(16))) char lq[QT * D * 2];
@@ -357,44 +357,46 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(AttnArgs a) {
         sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_b128(lq, roff[s] + u * RB), kf[s], sacc, 0, 0, 0);
         dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_b128(ldo, roff[s] + u * RB), vf[s], dpacc, 0, 0, 0);
       }
-      float lse4[16], del4[16];
+      uint32_t km = 0xFFFFu;   // bit r: P[row r] kept for this lane's key
+      if (DROP) {
+        // one hash per (query row, 4-key group): the quad's lanes (keys 4m..4m+3)
+        // each hash the rows r = 4g + lane&3, then broadcast within the quad (DPP);
+        // each broadcast hash is reduced to this lane's keep bit at once
+        km = 0;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int qr = q0 + 32 * u + 8 * g + 4 * h + kq;        // acc_row(4g + kq, h)
+          const int mine = (int)drop_hash(drop_rowbase(s32, row0 + qr), (uint32_t)key);
+          uint32_t hv[4];
+          hv[0] = (uint32_t)__builtin_amdgcn_mov_dpp(mine, 0x00, 0xF, 0xF, false);
+          hv[1] = (uint32_t)__builtin_amdgcn_mov_dpp(mine, 0x55, 0xF, 0xF, false);
+          hv[2] = (uint32_t)__builtin_amdgcn_mov_dpp(mine, 0xAA, 0xF, 0xF, false);
+          hv[3] = (uint32_t)__builtin_amdgcn_mov_dpp(mine, 0xFF, 0xF, 0xF, false);
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            km |= (((hv[j] >> (8 * kq)) & 0xFFu) >= dthr ? 1u : 0u) << (4 * g + j);
+        }
+      }
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const float4 a4 = *(const float4*)&llse[32 * u + 8 * g + 4 * h];
         const float4 b4 = *(const float4*)&ldel[32 * u + 8 * g + 4 * h];
-        lse4[4 * g] = a4.x; lse4[4 * g + 1] = a4.y; lse4[4 * g + 2] = a4.z; lse4[4 * g + 3] = a4.w;
-        del4[4 * g] = b4.x; del4[4 * g + 1] = b4.y; del4[4 * g + 2] = b4.z; del4[4 * g + 3] = b4.w;
-      }
-      uint32_t hsh[16];
-      if (DROP) {
-        // one hash per (query row, 4-key group): the quad's lanes (keys 4m..4m+3)
-        // each hash the rows r = 4g + lane&3, then broadcast within the quad (DPP)
-        uint32_t mine[4];
+        const float lse4[4] = {a4.x, a4.y, a4.z, a4.w};
+        const float del4[4] = {b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int qr = q0 + 32 * u + 8 * g + 4 * h + kq;        // acc_row(4g + kq, h)
-          mine[g] = drop_hash(drop_rowbase(s32, row0 + qr), (uint32_t)key);
+        for (int j = 0; j < 4; ++j) {
+          const int r = 4 * g + j;
+          const float p = __builtin_amdgcn_exp2f(fmaf(sacc[r], c, -lse4[j]));
+          float dp = dpacc[r];
+          if (DROP) {
+            const bool keep = (km >> r) & 1u;
+            dp = keep ? dp * ks : 0.f;
+            sacc[r] = keep ? p * ks : 0.f;   // dropped P feeds dV
+          } else {
+            sacc[r] = p;
+          }
+          dpacc[r] = p * (dp - del4[j]);     // dS
         }
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          hsh[4 * g + 0] = (uint32_t)__builtin_amdgcn_mov_dpp((int)mine[g], 0x00, 0xF, 0xF, false);
-          hsh[4 * g + 1] = (uint32_t)__builtin_amdgcn_mov_dpp((int)mine[g], 0x55, 0xF, 0xF, false);
-          hsh[4 * g + 2] = (uint32_t)__builtin_amdgcn_mov_dpp((int)mine[g], 0xAA, 0xF, 0xF, false);
-          hsh[4 * g + 3] = (uint32_t)__builtin_amdgcn_mov_dpp((int)mine[g], 0xFF, 0xF, 0xF, false);
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = __builtin_amdgcn_exp2f(fmaf(sacc[r], c, -lse4[r]));
-        float dp = dpacc[r];
-        if (DROP) {
-          const bool keep = ((hsh[r] >> (8 * kq)) & 0xFFu) >= dthr;
-          dp = keep ? dp * ks : 0.f;
-          sacc[r] = keep ? p * ks : 0.f;   // dropped P feeds dV
-        } else {
-          sacc[r] = p;
-        }
-        dpacc[r] = p * (dp - del4[r]);     // dS
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -427,7 +429,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(AttnArgs a) {
 // =============================================================== bf16 backward dQ
 // Queries on lanes; K / V tiles staged with prefetch; dQ^T = K^T dS^T.
 template <int D, bool DROP>
-__global__ __launch_bounds__(256) void attn_bwd_dq_bf16(AttnArgs a) {
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16(AttnArgs a) {
   constexpr int KT = 64;
   constexpr int RB = 32 * D * 2;
   __shared__ __attribute__((aligned(16))) char lk[KT * D * 2];
