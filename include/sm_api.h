@@ -64,6 +64,11 @@ int64_t sm_bn_workspace_bytes(int64_t M, int C);
 int sm_bn_stats(int x_dtype, int64_t M, int C, const void* x, float* mean, float* rstd,
                 float* run_mean, float* run_var, int64_t* num_batches_tracked, float momentum, float eps,
                 int updates, void* ws, int64_t ws_bytes, hipStream_t st);
+/* statistics from per-block partials [nrows][2][C] written by a fused producer */
+int64_t sm_bn_partials_workspace_bytes(int C);
+int sm_bn_stats_from_partials(const float* part, int64_t nrows, int C, int64_t M, float* mean, float* rstd,
+                              float* run_mean, float* run_var, int64_t* num_batches_tracked, float momentum,
+                              float eps, int updates, void* ws, int64_t ws_bytes, hipStream_t st);
 /* y = R + row_scale[row/rows_per_group] * act(BN(x)) (R / row_scale nullable: MBConv
  * residual with DropPath, tiny_vit.py:53-56) */
 int sm_bn_apply(int x_dtype, int y_dtype, int64_t M, int C, const void* x, const float* mean,
@@ -106,16 +111,36 @@ int sm_conv_wunpack_add(const float* packed, float* grad, int Cout, int Cin, int
 int sm_dwconv_fwd(int dtype, const void* x, const float* w, void* y, int F, int H, int W, int C,
                   int stride, hipStream_t st);
 int64_t sm_dwconv_wgrad_workspace_bytes(int F, int H, int W, int C, int stride);
+/* Fused MBConv depthwise path (tiny_vit.py:48-51, bf16): y = dwconv3x3(act(x)) with the
+ * producer's BN + GELU folded into the loads (in_mean == NULL: identity) and per-block
+ * BN statistics partials of y written to part[sm_dwconv_fused_partial_rows][2][C]
+ * (part nullable); backward: dx = dL/d act(x), dw += weight gradient with act(x)
+ * recomputed. C % 32 == 0, stride 1 or 2. */
+int64_t sm_dwconv_fused_partial_rows(int F, int H, int stride);
+int sm_dwconv_fused_fwd(int F, int H, int W, int C, int stride, const void* x, const float* in_mean,
+                        const float* in_rstd, const float* in_w, const float* in_b, int in_gelu,
+                        const float* w, void* y, float* part, hipStream_t st);
+int64_t sm_dwconv_fused_bwd_workspace_bytes(int F, int H, int W, int C, int stride);
+int sm_dwconv_fused_bwd(int F, int H, int W, int C, int stride, const void* dy, const void* x,
+                        const float* in_mean, const float* in_rstd, const float* in_w, const float* in_b,
+                        int in_gelu, const float* w, void* dx, float* dw, void* ws, int64_t ws_bytes,
+                        hipStream_t st);
 int sm_dwconv_bwd(int dtype, const void* dy, const void* x, const float* w, void* dx, float* dw, int F,
                   int H, int W, int C, int stride, void* ws, int64_t ws_bytes, hipStream_t st);
 
-/* ---- SELayer (tiny_vit.py:20-34) */
-int sm_se_fwd(int dtype, const void* x, int F, int HW, int C, int R, const float* w1, const float* w2,
-              float* pooled, float* z1, float* s, void* y, hipStream_t st);
-int sm_se_bwd(int dtype, const void* dy, const void* x, int F, int HW, int C, int R, const float* w1,
-              const float* w2, const float* s, const float* z1, float* ds_ws, float* dz2, float* dz1,
-              float* dpool_ws, void* dx, hipStream_t st);
-int sm_se_scale(int dtype, const void* x, const float* s, void* y, int F, int HW, int C, hipStream_t st);
+/* ---- SELayer (tiny_vit.py:20-34).  The SE input h = act(x) is recomputed from the
+ * pre-BatchNorm tensor x by every kernel that reads it (act = BN2 + GELU of MBConv,
+ * tiny_vit.py:50-51; act_mean == NULL: h = x). */
+int64_t sm_se_workspace_bytes(int F, int HW, int C);
+int sm_se_fwd(int dtype, const void* x, const float* act_mean, const float* act_rstd, const float* act_w,
+              const float* act_b, int act_gelu, int F, int HW, int C, int R, const float* w1, const float* w2,
+              float* pooled, float* z1, float* s, void* y, void* ws, int64_t ws_bytes, hipStream_t st);
+int sm_se_bwd(int dtype, const void* dy, const void* x, const float* act_mean, const float* act_rstd,
+              const float* act_w, const float* act_b, int act_gelu, int F, int HW, int C, int R,
+              const float* w1, const float* w2, const float* s, const float* z1, float* dz2, float* dz1,
+              void* dx, void* ws, int64_t ws_bytes, hipStream_t st);
+int sm_se_scale(int dtype, const void* x, const float* act_mean, const float* act_rstd, const float* act_w,
+                const float* act_b, int act_gelu, const float* s, void* y, int F, int HW, int C, hipStream_t st);
 
 /* ---- MAE glue: tube mask (mae_loader.py:80-90) + masked-token compaction
  * (train_ssl_mae.py:105), pos-embed/mask-token blend (mae_vit_adapter.py:97-104),

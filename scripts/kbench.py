@@ -89,9 +89,47 @@ def gemmk(args):
         torch.cuda.empty_cache()
 
 
+def mbconv(args):
+    """Stage-0 MBConv streaming ops at F = batch*8 frames of 112x112x384 (bf16)."""
+    Fn, H, W, C = args.batch * 8, 112, 112, 384
+    M = Fn * H * W
+    dev = "cuda"
+    a = (torch.randn(M, C, device=dev) * 2).to(torch.bfloat16)
+    g = torch.rand(C, device=dev) + 0.5
+    b = torch.randn(C, device=dev) * 0.1
+    m, r = K.bn_stats(a)
+    act = (m, r, g, b, True)
+    w = torch.randn(C, 9, device=dev) * 0.3
+
+    class BN:
+        running_mean = torch.zeros(C, device=dev)
+        running_var = torch.ones(C, device=dev)
+        num_batches_tracked = torch.zeros((), dtype=torch.int64, device=dev)
+        momentum, eps = 0.1, 1e-5
+    T = M * C * 2 / 1e9   # GB of one [M][C] bf16 tensor
+
+    def rep(name, ms, passes):
+        print(f"{name:28s} {ms:8.2f} ms  {passes * T / ms:6.2f} TB/s ({passes} passes of {T:.1f} GB)", flush=True)
+    rep("bn_stats", timeit(lambda: K.bn_stats(a), args.iters), 1)
+    rep("bn_apply+gelu", timeit(lambda: K.bn_apply(a, m, r, g, b, gelu=True), args.iters), 2)
+    y = K.dwconv_fused(a, act, w, Fn, H, W, C, 1)
+    rep("dwconv_fused s1 (+stats)", timeit(lambda: K.dwconv_fused(a, act, w, Fn, H, W, C, 1, bn_out=BN), args.iters), 2)
+    rep("dwconv_fused s1 no-act", timeit(lambda: K.dwconv_fused(a, None, w, Fn, H, W, C, 1), args.iters), 2)
+    dw = torch.zeros(C, 9, device=dev)
+    rep("dwconv_fused_bwd s1", timeit(lambda: K.dwconv_fused_bwd(y, a, act, w, dw, Fn, H, W, C, 1), args.iters), 4)
+    rep("dwconv_fused s2", timeit(lambda: K.dwconv_fused(a, act, w, Fn, H, W, C, 2), args.iters), 1.25)
+    w1 = torch.randn(C // 4, C, device=dev) * 0.1
+    w2 = torch.randn(C, C // 4, device=dev) * 0.1
+    _, _, h1, sg = K.se_fwd(a, Fn, H * W, C, w1, w2, act=act, want_y=False)
+    rep("se_fwd (act)", timeit(lambda: K.se_fwd(a, Fn, H * W, C, w1, w2, act=act), args.iters), 3)
+    rep("se_bwd (act)", timeit(lambda: K.se_bwd(y, a, Fn, H * W, C, w1, w2, sg, h1, act=act), args.iters), 4)
+    rep("bn_bwd gelu", timeit(lambda: K.bn_bwd(y, a, m, r, g, b, True, torch.zeros(C, device=dev),
+                                                torch.zeros(C, device=dev)), args.iters), 5)
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["attn", "gemm", "gemmk"])
+    ap.add_argument("what", choices=["attn", "gemm", "gemmk", "mbconv"])
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--drop", type=float, default=0.1)
     ap.add_argument("--iters", type=int, default=5)
@@ -99,4 +137,4 @@ if __name__ == "__main__":
     a = ap.parse_args()
     from ssl_mae_amd.build import build
     build()
-    {"attn": attn, "gemm": gemm, "gemmk": gemmk}[a.what](a)
+    {"attn": attn, "gemm": gemm, "gemmk": gemmk, "mbconv": mbconv}[a.what](a)

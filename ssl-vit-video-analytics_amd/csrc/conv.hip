@@ -258,6 +258,276 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(const T* dy, const float*
     if (xi0 + p < W) store8(dx + (((f * H + yi) * W + xi0 + p) * C + c8 * 8), acc[p]);
 }
 
+// ------------------------------------------------------------------ fused depthwise 3x3 (bf16)
+// y = dwconv3x3(act(x)) with act = the producer's BatchNorm + GELU folded per channel
+// (ChanAffine; identity when absent), plus per-frame BatchNorm statistics partials of
+// the bf16 output (part[f][2][C]: sum, sum of squares), so neither act(x) nor a
+// statistics pass over y touches HBM.
+// Block = (32-channel slice, frame).  It walks the frame in bands of TY output rows
+// through an LDS ring of NR = (TY-1)S+3 transformed input rows [NR][W+2][32] bf16
+// (zero border columns; rows outside the image are zero: the convolution pads
+// act(x)).  Each input row is transformed once; the TY*S new rows of band b+1 are
+// loaded into registers while band b is computed (software pipeline).  Every thread
+// computes PX = 7 consecutive outputs x 8 channels per item; odd PX keeps the 16-lane
+// groups of ds_read_b128 conflict-free (strip pitch 448 B).  Taps accumulate in the
+// (ky, kx) order of dw_fwd_kernel: bit-identical y.
+constexpr int DWF_CB = 32, DWF_PX = 7, DWF_KV = 7;
+
+template <int S>
+constexpr int dwf_ty() { return S == 1 ? 4 : 2; }
+
+template <int S>
+struct DwRing {
+  static constexpr int TY = dwf_ty<S>();
+  static constexpr int NR = (TY - 1) * S + 3;
+  static constexpr int NEW = TY * S;              // rows entering the ring per band
+  const __bf16* x;
+  int64_t f;
+  int H, W, C, cbase, c8, pitch;
+  uint4 raw[DWF_KV];
+  SM_DEV int slot(int iy) const { return (iy + 1 + NR) % NR; }
+  // raw-load rows [iy_first, iy_first + nrows) (nrows * W * 4 <= 256 * DWF_KV)
+  SM_DEV void load(int iy_first, int nrows) {
+    const int t = threadIdx.x;
+    const int nvec = nrows * W * 4;
+#pragma unroll
+    for (int k = 0; k < DWF_KV; ++k) {
+      const int v = t + 256 * k;
+      const int q = v >> 2;
+      const int r = q / W, xx = q - r * W;
+      const int iy = iy_first + r;
+      raw[k] = make_uint4(0, 0, 0, 0);
+      if (v < nvec && iy >= 0 && iy < H) raw[k] = *(const uint4*)(x + ((f * H + iy) * W + xx) * C + cbase);
+    }
+  }
+  SM_DEV void commit(char* lds, const Affine8& af, int iy_first, int nrows) const {
+    const int t = threadIdx.x;
+    const int nvec = nrows * W * 4;
+#pragma unroll
+    for (int k = 0; k < DWF_KV; ++k) {
+      const int v = t + 256 * k;
+      if (v >= nvec) break;
+      const int q = v >> 2;
+      const int r = q / W, xx = q - r * W;
+      const int iy = iy_first + r;
+      float a[8];
+      if (iy >= 0 && iy < H) {
+        load8((const __bf16*)&raw[k], a);
+        af.apply<__bf16>(a);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] = 0.f;
+      }
+      store8((__bf16*)(lds + slot(iy) * pitch + (xx + 1) * 64 + c8 * 16), a);
+    }
+  }
+  SM_DEV void zero_borders(char* lds) const {
+    const int t = threadIdx.x;
+    if (t < NR * 8) {
+      const int r = t >> 3, side = (t >> 2) & 1;
+      *(uint4*)(lds + r * pitch + (side ? W + 1 : 0) * 64 + c8 * 16) = make_uint4(0, 0, 0, 0);
+    }
+  }
+  // the first band's NR rows (from iy0 = -1), in two register batches
+  SM_DEV void stage_first(char* lds, const Affine8& af) {
+    const int first = (NR + 1) / 2;
+    load(-1, first);
+    commit(lds, af, -1, first);
+    load(-1 + first, NR - first);
+    commit(lds, af, -1 + first, NR - first);
+    zero_borders(lds);
+  }
+};
+
+template <int S>
+__global__ __launch_bounds__(256, 2) void dwf_fwd_kernel(const __bf16* x, ChanAffine act, const float* w,
+                                                         __bf16* y, float* part, int H, int W, int C, int Ho,
+                                                         int Wo) {
+  using R = DwRing<S>;
+  constexpr int TY = R::TY;
+  constexpr int PX = DWF_PX;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int cs = blockIdx.x;
+  const int64_t f = blockIdx.y;
+  const int t = threadIdx.x;
+  const int c8 = t & 3;
+  const int cbase = cs * DWF_CB + c8 * 8;
+  R ring{x, f, H, W, C, cbase, c8, (W + 2) * 64};
+  Affine8 af;
+  af.init(act, cbase);
+  // taps in LDS after the ring ([9][32] fp32), re-read per row of taps: keeps the
+  // 72 weights out of the register file (occupancy); 6 ds_read_b128 per item row
+  float* wl = (float*)(lds + R::NR * ring.pitch);
+  for (int i = t; i < 9 * DWF_CB; i += 256) {
+    const int tap = i / DWF_CB, ch = i % DWF_CB;
+    wl[i] = w[(int64_t)(cs * DWF_CB + ch) * 9 + tap];
+  }
+  float s8[8], q8[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { s8[j] = 0.f; q8[j] = 0.f; }
+  const int nstrip = (Wo + PX - 1) / PX;
+  const int items = TY * nstrip * 4;
+  const int nbands = (Ho + TY - 1) / TY;
+  ring.stage_first(lds, af);
+  for (int band = 0; band < nbands; ++band) {
+    const int yo0 = band * TY;
+    if (band > 0) {
+      __syncthreads();                                  // band-1 finished reading the slots we overwrite
+      ring.commit(lds, af, (yo0 * S - 1) + (3 - S), R::NEW);
+    }
+    __syncthreads();
+    if (band + 1 < nbands) ring.load(((yo0 + TY) * S - 1) + (3 - S), R::NEW);   // next band, in flight
+    for (int it = t; it < items; it += 256) {
+      const int q = it >> 2;
+      const int ry = q / nstrip, strip = q - ry * nstrip;
+      const int yo = yo0 + ry;
+      if (yo >= Ho) continue;
+      const int xo0 = strip * PX;
+      float acc[PX][8];
+#pragma unroll
+      for (int p = 0; p < PX; ++p)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[p][j] = 0.f;
+      const float* wlt = wl + c8 * 8;
+      asm volatile("" : "+v"(wlt));             // per-item reload: do not hoist the taps
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        const char* rowp = lds + ring.slot(yo * S - 1 + ky) * ring.pitch + c8 * 16;
+        float wr[3][8];
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) load8(wlt + (ky * 3 + kx) * DWF_CB, wr[kx]);
+#pragma unroll
+        for (int ci = 0; ci < (PX - 1) * S + 3; ++ci) {
+          const int col = xo0 * S + ci;          // LDS column = input x + 1
+          if (col > W + 1) break;                // ragged last strip
+          float v[8];
+          load8((const __bf16*)(rowp + col * 64), v);
+#pragma unroll
+          for (int p = 0; p < PX; ++p) {
+            const int kx = ci - p * S;
+            if (kx < 0 || kx > 2) continue;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[p][j] += v[j] * wr[kx][j];
+          }
+        }
+      }
+#pragma unroll
+      for (int p = 0; p < PX; ++p) {
+        if (xo0 + p >= Wo) break;
+        float r8[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          r8[j] = (float)(__bf16)acc[p][j];
+          s8[j] += r8[j];
+          q8[j] += r8[j] * r8[j];
+        }
+        store8(y + ((f * Ho + yo) * Wo + xo0 + p) * C + cbase, r8);
+      }
+    }
+  }
+  if (!part) return;
+  __syncthreads();                              // ring dead: reuse for the reduction
+  float* red = (float*)lds;                     // [256][16]
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { red[t * 16 + j] = s8[j]; red[t * 16 + 8 + j] = q8[j]; }
+  __syncthreads();
+  if (t < 2 * DWF_CB) {
+    const int ch = t & (DWF_CB - 1), which = t / DWF_CB;
+    const int g = ch >> 3, j = ch & 7;
+    float a = 0.f;
+    for (int k = 0; k < 64; ++k) a += red[(k * 4 + g) * 16 + which * 8 + j];
+    part[(f * 2 + which) * C + cs * DWF_CB + ch] = a;
+  }
+}
+
+// Fused depthwise weight gradient: dw[c][tap] = sum dy[yo][xo][c] * act(x)[yo*S+ky-1][xo*S+kx-1][c]
+// with act(x) recomputed through the same ring as dwf_fwd_kernel (and the same
+// register prefetch of the next band).  Block = (32-channel slice, frame); the 72
+// (tap, channel) sums of each thread stay in registers over the frame, then reduce
+// over the 64 threads that share its 8 channels: part[f][C][9] (colred over frames).
+template <int S>
+__global__ __launch_bounds__(256, 2) void dwf_wgrad_kernel(const __bf16* dy, const __bf16* x, ChanAffine act,
+                                                           float* part, int H, int W, int C, int Ho, int Wo) {
+  using R = DwRing<S>;
+  constexpr int TY = R::TY;
+  constexpr int PX = DWF_PX;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int cs = blockIdx.x;
+  const int64_t f = blockIdx.y;
+  const int t = threadIdx.x;
+  const int c8 = t & 3;
+  const int cbase = cs * DWF_CB + c8 * 8;
+  R ring{x, f, H, W, C, cbase, c8, (W + 2) * 64};
+  Affine8 af;
+  af.init(act, cbase);
+  float acc[9][8];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[k][j] = 0.f;
+  const int nstrip = (Wo + PX - 1) / PX;
+  const int items = TY * nstrip * 4;
+  const int nbands = (Ho + TY - 1) / TY;
+  ring.stage_first(lds, af);
+  for (int band = 0; band < nbands; ++band) {
+    const int yo0 = band * TY;
+    if (band > 0) {
+      __syncthreads();
+      ring.commit(lds, af, (yo0 * S - 1) + (3 - S), R::NEW);
+    }
+    __syncthreads();
+    if (band + 1 < nbands) ring.load(((yo0 + TY) * S - 1) + (3 - S), R::NEW);
+    for (int it = t; it < items; it += 256) {
+      const int q = it >> 2;
+      const int ry = q / nstrip, strip = q - ry * nstrip;
+      const int yo = yo0 + ry;
+      if (yo >= Ho) continue;
+      const int xo0 = strip * PX;
+      float g[PX][8];
+#pragma unroll
+      for (int p = 0; p < PX; ++p) {
+        if (xo0 + p < Wo) load8(dy + ((f * Ho + yo) * Wo + xo0 + p) * C + cbase, g[p]);
+        else
+#pragma unroll
+          for (int j = 0; j < 8; ++j) g[p][j] = 0.f;
+      }
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        const char* rowp = lds + ring.slot(yo * S - 1 + ky) * ring.pitch + c8 * 16;
+#pragma unroll
+        for (int ci = 0; ci < (PX - 1) * S + 3; ++ci) {
+          const int col = xo0 * S + ci;
+          if (col > W + 1) break;
+          float v[8];
+          load8((const __bf16*)(rowp + col * 64), v);
+#pragma unroll
+          for (int p = 0; p < PX; ++p) {
+            const int kx = ci - p * S;
+            if (kx < 0 || kx > 2) continue;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[ky * 3 + kx][j] += g[p][j] * v[j];
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  float* red = (float*)lds;   // [256][8] per tap
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[t * 8 + j] = acc[tap][j];
+    __syncthreads();
+    if (t < DWF_CB) {
+      const int g = t >> 3, j = t & 7;
+      float a = 0.f;
+      for (int k = 0; k < 64; ++k) a += red[(k * 4 + g) * 8 + j];
+      part[(f * C + cs * DWF_CB + t) * 9 + tap] = a;
+    }
+    __syncthreads();
+  }
+}
+
 // partial dw per block: part[blk][C][9]
 template <typename T>
 __global__ __launch_bounds__(256) void dw_wgrad_kernel(const T* dy, const T* x, int F, int H, int W, int C, int Ho,
@@ -320,41 +590,79 @@ __global__ void colsum_add_kernel(const float* part, int nb, int n, float* out) 
 }
 
 // ------------------------------------------------------------------ SE
-// pooled[f][c] = mean_hw x[f][hw][c]   (block per frame)
+// The SE input h = act(x) (the BN2 + GELU of MBConv, ChanAffine) is recomputed in
+// every kernel that reads it instead of being materialised.  Frame reductions are
+// split over nsplit pixel ranges per frame (grid (nsplit, F)) into partial slabs
+// part[f][k][C], summed in fixed order by the per-frame FC kernels.  Thread layout:
+// Col8 (8 channels per thread, 16-B loads, per-channel constants in registers).
+constexpr int SE_PX_PER_SPLIT = 784;
+
+__host__ __device__ inline int se_splits(int HW) { return (HW + SE_PX_PER_SPLIT - 1) / SE_PX_PER_SPLIT; }
+
+struct SeCols {
+  int nch, rpp, c0, r;
+  SM_DEV SeCols(int C) {
+    nch = C / 8;
+    rpp = 256 / nch;
+    c0 = (threadIdx.x % nch) * 8;
+    r = threadIdx.x / nch;
+  }
+};
+
+// part[f][k][c] = sum over split k of h  (h = act(x))      or of dy * h when dy
 template <typename T>
-__global__ __launch_bounds__(256) void se_pool_kernel(const T* x, int HW, int C, float* pooled) {
-  __shared__ float red[256 * 4];
-  const int nch = C / 4;
-  const int rpp = 256 / nch;
-  const int ch = threadIdx.x % nch, r = threadIdx.x / nch;
-  const int64_t f = blockIdx.x;
-  float s[4] = {0, 0, 0, 0};
-  if (r < rpp)
-    for (int p = r; p < HW; p += rpp) {
-      float v[4];
-      load4(x + ((f * HW + p) * C + ch * 4), v);
+__global__ __launch_bounds__(256) void se_reduce_kernel(const T* x, const T* dy, ChanAffine act, int HW, int C,
+                                                        float* part) {
+  __shared__ float red[256 * 8];
+  const SeCols cm(C);
+  const int k = blockIdx.x, nsplit = gridDim.x;
+  const int64_t f = blockIdx.y;
+  const int p0 = k * SE_PX_PER_SPLIT, p1 = min(HW, p0 + SE_PX_PER_SPLIT);
+  float s[8];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) s[j] += v[j];
+  for (int j = 0; j < 8; ++j) s[j] = 0.f;
+  if (cm.r < cm.rpp) {
+    Affine8 af;
+    af.init(act, cm.c0);
+    for (int p = p0 + cm.r; p < p1; p += cm.rpp) {
+      const int64_t e = (f * HW + p) * C + cm.c0;
+      float v[8];
+      load8(x + e, v);
+      af.apply<T>(v);
+      if (dy) {
+        float g[8];
+        load8(dy + e, g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] *= g[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += v[j];
     }
+  }
 #pragma unroll
-  for (int j = 0; j < 4; ++j) red[threadIdx.x * 4 + j] = s[j];
+  for (int j = 0; j < 8; ++j) red[threadIdx.x * 8 + j] = s[j];
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += 256) {
     float a = 0.f;
-    for (int rr = 0; rr < rpp; ++rr) a += red[(rr * nch + c / 4) * 4 + c % 4];
-    pooled[f * C + c] = a / HW;
+    for (int rr = 0; rr < cm.rpp; ++rr) a += red[(rr * cm.nch + c / 8) * 8 + c % 8];
+    part[(f * nsplit + k) * C + c] = a;
   }
 }
 
-// per frame: z1 = W1 p; h1 = relu(z1); z2 = W2 h1; s = sigmoid(z2)
-__global__ __launch_bounds__(256) void se_fc_fwd_kernel(const float* pooled, const float* w1 /*[R][C]*/,
-                                                        const float* w2 /*[C][R]*/, int C, int R, float* h1_out,
-                                                        float* s_out) {
+// per frame: p = sum_k part / HW; z1 = W1 p; h1 = relu(z1); z2 = W2 h1; s = sigmoid(z2)
+__global__ __launch_bounds__(256) void se_fc_fwd_kernel(const float* part, int nsplit, int HW,
+                                                        const float* w1 /*[R][C]*/, const float* w2 /*[C][R]*/,
+                                                        int C, int R, float* pooled, float* h1_out, float* s_out) {
   extern __shared__ float sh[];
   float* p = sh;          // C
   float* h = sh + C;      // R
   const int64_t f = blockIdx.x;
-  for (int c = threadIdx.x; c < C; c += 256) p[c] = pooled[f * C + c];
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float a = 0.f;
+    for (int k = 0; k < nsplit; ++k) a += part[(f * nsplit + k) * C + c];
+    p[c] = a / HW;
+    pooled[f * C + c] = p[c];
+  }
   __syncthreads();
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   for (int j = w; j < R; j += 4) {
@@ -371,60 +679,50 @@ __global__ __launch_bounds__(256) void se_fc_fwd_kernel(const float* pooled, con
   }
 }
 
-// y = x * s[f][c]
+// y = act(x) * s[f][c]          (dpool == null)
+// y = x * s[f][c] + dpool[f][c] / HW   (backward dx, x = dy, act identity)
 template <typename T>
-__global__ void se_scale_kernel(const T* x, const float* s, T* y, int64_t HW, int C, int64_t total8) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total8; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t e = i * 8;
-    const int64_t f = e / (HW * C);
-    const int c0 = (int)(e % C);
+__global__ __launch_bounds__(256) void se_apply_kernel(const T* x, ChanAffine act, const float* s,
+                                                       const float* dpool, T* y, int HW, int C) {
+  const SeCols cm(C);
+  if (cm.r >= cm.rpp) return;
+  const int k = blockIdx.x;
+  const int64_t f = blockIdx.y;
+  const int p0 = k * SE_PX_PER_SPLIT, p1 = min(HW, p0 + SE_PX_PER_SPLIT);
+  Affine8 af;
+  af.init(act, cm.c0);
+  float sc[8], add[8];
+  const float inv = 1.f / (float)HW;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = s[f * C + cm.c0 + j];
+    add[j] = dpool ? dpool[f * C + cm.c0 + j] * inv : 0.f;
+  }
+  for (int p = p0 + cm.r; p < p1; p += cm.rpp) {
+    const int64_t e = (f * HW + p) * C + cm.c0;
     float v[8];
     load8(x + e, v);
+    af.apply<T>(v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] *= s[f * C + c0 + j];
+    for (int j = 0; j < 8; ++j) v[j] = dpool ? v[j] * sc[j] + add[j] : v[j] * sc[j];
     store8(y + e, v);
   }
 }
 
-// ds[f][c] = sum_hw dy * x      (block per frame)
-template <typename T>
-__global__ __launch_bounds__(256) void se_dscale_kernel(const T* dy, const T* x, int HW, int C, float* ds) {
-  __shared__ float red[256 * 4];
-  const int nch = C / 4;
-  const int rpp = 256 / nch;
-  const int ch = threadIdx.x % nch, r = threadIdx.x / nch;
-  const int64_t f = blockIdx.x;
-  float s[4] = {0, 0, 0, 0};
-  if (r < rpp)
-    for (int p = r; p < HW; p += rpp) {
-      float a[4], b[4];
-      load4(dy + ((f * HW + p) * C + ch * 4), a);
-      load4(x + ((f * HW + p) * C + ch * 4), b);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) s[j] += a[j] * b[j];
-    }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) red[threadIdx.x * 4 + j] = s[j];
-  __syncthreads();
-  for (int c = threadIdx.x; c < C; c += 256) {
-    float a = 0.f;
-    for (int rr = 0; rr < rpp; ++rr) a += red[(rr * nch + c / 4) * 4 + c % 4];
-    ds[f * C + c] = a;
-  }
-}
-
-// per frame backward through sigmoid / W2 / relu / W1:
+// per frame backward through sigmoid / W2 / relu / W1 (ds = sum_k part):
 //   dz2 = ds * s (1-s);  dh1 = W2^T dz2;  dz1 = dh1 * (z1 > 0);  dpool = W1^T dz1
-__global__ __launch_bounds__(256) void se_fc_bwd_kernel(const float* ds, const float* s, const float* z1,
-                                                        const float* w1, const float* w2, int C, int R,
-                                                        float* dz2_out, float* dz1_out, float* dpool) {
+__global__ __launch_bounds__(256) void se_fc_bwd_kernel(const float* part, int nsplit, const float* s,
+                                                        const float* z1, const float* w1, const float* w2, int C,
+                                                        int R, float* dz2_out, float* dz1_out, float* dpool) {
   extern __shared__ float sh[];
   float* dz2 = sh;      // C
   float* dz1 = sh + C;  // R
   const int64_t f = blockIdx.x;
   for (int c = threadIdx.x; c < C; c += 256) {
+    float ds = 0.f;
+    for (int k = 0; k < nsplit; ++k) ds += part[(f * nsplit + k) * C + c];
     const float sv = s[f * C + c];
-    const float g = ds[f * C + c] * sv * (1.f - sv);
+    const float g = ds * sv * (1.f - sv);
     dz2[c] = g;
     dz2_out[f * C + c] = g;
   }
@@ -445,23 +743,6 @@ __global__ __launch_bounds__(256) void se_fc_bwd_kernel(const float* ds, const f
     float a = 0.f;
     for (int j = 0; j < R; ++j) a += w1[(int64_t)j * C + c] * dz1[j];
     dpool[f * C + c] = a;
-  }
-}
-
-// dx = dy * s + dpool / HW
-template <typename T>
-__global__ void se_dx_kernel(const T* dy, const float* s, const float* dpool, T* dx, int64_t HW, int C,
-                             int64_t total8) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total8; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t e = i * 8;
-    const int64_t f = e / (HW * C);
-    const int c0 = (int)(e % C);
-    float v[8];
-    load8(dy + e, v);
-    const float inv = 1.f / (float)HW;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = v[j] * s[f * C + c0 + j] + dpool[f * C + c0 + j] * inv;
-    store8(dx + e, v);
   }
 }
 
@@ -546,6 +827,86 @@ extern "C" int sm_dwconv_fwd(int dtype, const void* x, const float* w, void* y, 
   return 0;
 }
 
+static size_t dwf_lds_bytes(int W, int stride) {
+  const int NR = stride == 1 ? DwRing<1>::NR : DwRing<2>::NR;
+  size_t lds = (size_t)NR * (W + 2) * 64 + 9 * DWF_CB * 4;   // ring + taps
+  return lds < 256 * 16 * 4 ? 256 * 16 * 4 : lds;   // the statistics reduction reuses it
+}
+
+static bool dwf_shape_ok(int F, int W, int C, int stride) {
+  return C % DWF_CB == 0 && (stride == 1 || stride == 2) && F > 0 && F <= 65535 &&
+         DwRing<2>::NEW * W * 4 <= 256 * DWF_KV && DwRing<1>::NEW * W * 4 <= 256 * DWF_KV &&
+         dwf_lds_bytes(W, stride) <= 64 * 1024;
+}
+
+extern "C" int64_t sm_dwconv_fused_partial_rows(int F, int H, int stride) { return F; }
+
+extern "C" int sm_dwconv_fused_fwd(int F, int H, int W, int C, int stride, const void* x, const float* in_mean,
+                                   const float* in_rstd, const float* in_w, const float* in_b, int in_gelu,
+                                   const float* w, void* y, float* part, hipStream_t st) {
+  if (!dwf_shape_ok(F, W, C, stride)) return -2;
+  if (((uintptr_t)w & 15) || ((uintptr_t)x & 15) || ((uintptr_t)y & 15)) return -2;
+  const int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
+  ChanAffine act{in_mean, in_rstd, in_w, in_b, in_gelu};
+  dim3 grid(C / DWF_CB, F);
+  const size_t lds = dwf_lds_bytes(W, stride);
+  if (stride == 1)
+    hipLaunchKernelGGL((dwf_fwd_kernel<1>), grid, dim3(256), lds, st, (const __bf16*)x, act, w, (__bf16*)y, part,
+                       H, W, C, Ho, Wo);
+  else
+    hipLaunchKernelGGL((dwf_fwd_kernel<2>), grid, dim3(256), lds, st, (const __bf16*)x, act, w, (__bf16*)y, part,
+                       H, W, C, Ho, Wo);
+  SM_CHECK_LAUNCH();
+  return 0;
+}
+
+// Fused backward of y = dwconv(act(x)): dx = dL/d act(x) (stride 1: the forward
+// kernel with the taps rotated 180 degrees; stride 2: dw_dgrad_kernel), dw += the
+// fused weight gradient.
+__global__ void dw_rotate_kernel(const float* w, float* wrot, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) wrot[i] = w[(i / 9) * 9 + 8 - i % 9];
+}
+
+extern "C" int64_t sm_dwconv_fused_bwd_workspace_bytes(int F, int H, int W, int C, int stride) {
+  return (int64_t)F * C * 9 * 4 + (int64_t)C * 9 * 4 + 64;
+}
+
+extern "C" int sm_dwconv_fused_bwd(int F, int H, int W, int C, int stride, const void* dy, const void* x,
+                                   const float* in_mean, const float* in_rstd, const float* in_w, const float* in_b,
+                                   int in_gelu, const float* w, void* dx, float* dw, void* ws, int64_t ws_bytes,
+                                   hipStream_t st) {
+  if (!dwf_shape_ok(F, W, C, stride)) return -2;
+  if (ws_bytes < sm_dwconv_fused_bwd_workspace_bytes(F, H, W, C, stride)) return -4;
+  const int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
+  const size_t lds = dwf_lds_bytes(W, stride);
+  float* part = (float*)ws;
+  float* wrot = (float*)(((uintptr_t)(part + (int64_t)F * C * 9) + 15) & ~(uintptr_t)15);
+  if (dx) {
+    if (stride == 1) {
+      hipLaunchKernelGGL(dw_rotate_kernel, dim3((C * 9 + 255) / 256), dim3(256), 0, st, w, wrot, C * 9);
+      ChanAffine none{nullptr, nullptr, nullptr, nullptr, 0};
+      hipLaunchKernelGGL((dwf_fwd_kernel<1>), dim3(C / DWF_CB, F), dim3(256), lds, st, (const __bf16*)dy, none,
+                         (const float*)wrot, (__bf16*)dx, (float*)nullptr, Ho, Wo, C, H, W);
+    } else {
+      const int64_t total = (int64_t)F * H * ((W + DW_PX - 1) / DW_PX) * (C / 8);
+      hipLaunchKernelGGL((dw_dgrad_kernel<__bf16, 2>), dim3((int)((total + 255) / 256)), dim3(256), 0, st,
+                         (const __bf16*)dy, w, (__bf16*)dx, F, H, W, C, Ho, Wo);
+    }
+  }
+  ChanAffine act{in_mean, in_rstd, in_w, in_b, in_gelu};
+  dim3 g2(C / DWF_CB, F);
+  if (stride == 1)
+    hipLaunchKernelGGL((dwf_wgrad_kernel<1>), g2, dim3(256), lds, st, (const __bf16*)dy, (const __bf16*)x, act, part,
+                       H, W, C, Ho, Wo);
+  else
+    hipLaunchKernelGGL((dwf_wgrad_kernel<2>), g2, dim3(256), lds, st, (const __bf16*)dy, (const __bf16*)x, act, part,
+                       H, W, C, Ho, Wo);
+  colred(part, F, C * 9, nullptr, dw, 1, st);
+  SM_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int64_t sm_dwconv_wgrad_workspace_bytes(int F, int H, int W, int C, int stride) {
   const int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
   const int64_t P = (int64_t)F * Ho * Wo;
@@ -584,41 +945,62 @@ extern "C" int sm_dwconv_bwd(int dtype, const void* dy, const void* x, const flo
   return 0;
 }
 
-extern "C" int sm_se_fwd(int dtype, const void* x, int F, int HW, int C, int R, const float* w1, const float* w2,
-                         float* pooled, float* z1, float* s, void* y, hipStream_t st) {
-  if (C % 8 || C / 4 > 256) return -2;
-  DISPATCH1(dtype, hipLaunchKernelGGL(se_pool_kernel<T>, dim3(F), dim3(256), 0, st, (const T*)x, HW, C, pooled));
-  hipLaunchKernelGGL(se_fc_fwd_kernel, dim3(F), dim3(256), (C + R) * 4, st, pooled, w1, w2, C, R, z1, s);
-  const int64_t n8 = (int64_t)F * HW * C / 8;
-  DISPATCH1(dtype, hipLaunchKernelGGL(se_scale_kernel<T>, dim3(ew_blocks(n8)), dim3(256), 0, st, (const T*)x, s,
-                                      (T*)y, (int64_t)HW, C, n8));
+extern "C" int64_t sm_se_workspace_bytes(int F, int HW, int C) {
+  return (int64_t)F * se_splits(HW) * C * 4 + (int64_t)F * C * 4 + 64;
+}
+
+// y = act(x) * sigmoid(W2 relu(W1 mean_hw act(x)))  (y nullable: gate only)
+extern "C" int sm_se_fwd(int dtype, const void* x, const float* act_mean, const float* act_rstd, const float* act_w,
+                         const float* act_b, int act_gelu, int F, int HW, int C, int R, const float* w1,
+                         const float* w2, float* pooled, float* z1, float* s, void* y, void* ws, int64_t ws_bytes,
+                         hipStream_t st) {
+  if (C % 8 || C / 8 > 256 || F <= 0 || F > 65535 || HW <= 0) return -2;
+  const int ns = se_splits(HW);
+  if (ws_bytes < (int64_t)F * ns * C * 4) return -4;
+  float* part = (float*)ws;
+  ChanAffine act{act_mean, act_rstd, act_w, act_b, act_gelu};
+  DISPATCH1(dtype, hipLaunchKernelGGL(se_reduce_kernel<T>, dim3(ns, F), dim3(256), 0, st, (const T*)x,
+                                      (const T*)nullptr, act, HW, C, part));
+  hipLaunchKernelGGL(se_fc_fwd_kernel, dim3(F), dim3(256), (C + R) * 4, st, part, ns, HW, w1, w2, C, R, pooled, z1,
+                     s);
+  if (y)
+    DISPATCH1(dtype, hipLaunchKernelGGL(se_apply_kernel<T>, dim3(ns, F), dim3(256), 0, st, (const T*)x, act, s,
+                                        (const float*)nullptr, (T*)y, HW, C));
   SM_CHECK_LAUNCH();
   return 0;
 }
 
-// Backward of y = x * sigmoid(W2 relu(W1 mean_hw(x))).  Writes dx and the per-frame
-// FC gradients dz2 [F][C], dz1 [F][R] (the weight grads are two small GEMMs).
-extern "C" int sm_se_bwd(int dtype, const void* dy, const void* x, int F, int HW, int C, int R, const float* w1,
-                         const float* w2, const float* s, const float* z1, float* ds_ws, float* dz2, float* dz1,
-                         float* dpool_ws, void* dx, hipStream_t st) {
-  if (C % 8 || C / 4 > 256) return -2;
-  DISPATCH1(dtype, hipLaunchKernelGGL(se_dscale_kernel<T>, dim3(F), dim3(256), 0, st, (const T*)dy, (const T*)x,
-                                      HW, C, ds_ws));
-  hipLaunchKernelGGL(se_fc_bwd_kernel, dim3(F), dim3(256), (C + R) * 4, st, ds_ws, s, z1, w1, w2, C, R, dz2, dz1,
-                     dpool_ws);
-  const int64_t n8 = (int64_t)F * HW * C / 8;
-  DISPATCH1(dtype, hipLaunchKernelGGL(se_dx_kernel<T>, dim3(ew_blocks(n8)), dim3(256), 0, st, (const T*)dy, s,
-                                      dpool_ws, (T*)dx, (int64_t)HW, C, n8));
+// Backward of y = h * s(h), h = act(x).  Writes dx = dL/dh and the per-frame FC
+// gradients dz2 [F][C], dz1 [F][R] (the weight grads are two small GEMMs).
+extern "C" int sm_se_bwd(int dtype, const void* dy, const void* x, const float* act_mean, const float* act_rstd,
+                         const float* act_w, const float* act_b, int act_gelu, int F, int HW, int C, int R,
+                         const float* w1, const float* w2, const float* s, const float* z1, float* dz2, float* dz1,
+                         void* dx, void* ws, int64_t ws_bytes, hipStream_t st) {
+  if (C % 8 || C / 8 > 256 || F <= 0 || F > 65535 || HW <= 0) return -2;
+  const int ns = se_splits(HW);
+  if (ws_bytes < (int64_t)F * ns * C * 4 + (int64_t)F * C * 4) return -4;
+  float* part = (float*)ws;
+  float* dpool = part + (int64_t)F * ns * C;
+  ChanAffine act{act_mean, act_rstd, act_w, act_b, act_gelu};
+  ChanAffine none{nullptr, nullptr, nullptr, nullptr, 0};
+  DISPATCH1(dtype, hipLaunchKernelGGL(se_reduce_kernel<T>, dim3(ns, F), dim3(256), 0, st, (const T*)x,
+                                      (const T*)dy, act, HW, C, part));
+  hipLaunchKernelGGL(se_fc_bwd_kernel, dim3(F), dim3(256), (C + R) * 4, st, part, ns, s, z1, w1, w2, C, R, dz2, dz1,
+                     dpool);
+  DISPATCH1(dtype, hipLaunchKernelGGL(se_apply_kernel<T>, dim3(ns, F), dim3(256), 0, st, (const T*)dy, none, s,
+                                      (const float*)dpool, (T*)dx, HW, C));
   SM_CHECK_LAUNCH();
   return 0;
 }
 
-extern "C" int sm_se_scale(int dtype, const void* x, const float* s, void* y, int F, int HW, int C, hipStream_t st) {
-  if (C % 8) return -2;
-  const int64_t n8 = (int64_t)F * HW * C / 8;
-  if (n8 <= 0) return 0;
-  DISPATCH1(dtype, hipLaunchKernelGGL(se_scale_kernel<T>, dim3(ew_blocks(n8)), dim3(256), 0, st, (const T*)x, s,
-                                      (T*)y, (int64_t)HW, C, n8));
+extern "C" int sm_se_scale(int dtype, const void* x, const float* act_mean, const float* act_rstd,
+                           const float* act_w, const float* act_b, int act_gelu, const float* s, void* y, int F,
+                           int HW, int C, hipStream_t st) {
+  if (C % 8 || C / 8 > 256 || F > 65535) return -2;
+  if (F <= 0 || HW <= 0) return 0;
+  ChanAffine act{act_mean, act_rstd, act_w, act_b, act_gelu};
+  DISPATCH1(dtype, hipLaunchKernelGGL(se_apply_kernel<T>, dim3(se_splits(HW), F), dim3(256), 0, st, (const T*)x,
+                                      act, s, (const float*)nullptr, (T*)y, HW, C));
   SM_CHECK_LAUNCH();
   return 0;
 }

@@ -196,7 +196,7 @@ __global__ void bn_finalize_kernel(const double* sums /*[2][C]*/, const T* x, in
   if (c == 0 && nbt) *nbt += updates;
   if (c >= C) return;
   const double s = sums[c], q = sums[C + c];
-  const double shift = (double)to_f<T>(x[c]);
+  const double shift = x ? (double)to_f<T>(x[c]) : 0.0;   // null: unshifted partials
   const double md = s / (double)M;
   double var = q / (double)M - md * md;
   if (var < 0) var = 0;
@@ -580,6 +580,26 @@ extern "C" int sm_bn_stats(int x_dtype, int64_t M, int C, const void* x, float* 
                        (const float*)x, M, C, eps, momentum, mean, rstd, run_mean, run_var, updates,
                        num_batches_tracked);
   }
+  SM_CHECK_LAUNCH();
+  return 0;
+}
+
+// BatchNorm statistics from per-block partials [nrows][2][C] (sum, sum of squares,
+// unshifted) produced inside another kernel (e.g. the fused depthwise conv): fixed-order
+// fp64 column reduction + the same finalize / running-stat update as sm_bn_stats.
+extern "C" int64_t sm_bn_partials_workspace_bytes(int C) { return (int64_t)2 * C * 8; }
+
+extern "C" int sm_bn_stats_from_partials(const float* part, int64_t nrows, int C, int64_t M, float* mean,
+                                         float* rstd, float* run_mean, float* run_var, int64_t* num_batches_tracked,
+                                         float momentum, float eps, int updates, void* ws, int64_t ws_bytes,
+                                         hipStream_t st) {
+  if (M <= 0 || nrows <= 0 || nrows > 0x7fffffff) return -2;
+  if (ws_bytes < (int64_t)2 * C * 8) return -4;
+  double* sums = (double*)ws;
+  colred(part, (int)nrows, 2 * C, sums, nullptr, 0, st);
+  hipLaunchKernelGGL(bn_finalize_kernel<__bf16>, dim3((C + 127) / 128), dim3(128), 0, st, sums,
+                     (const __bf16*)nullptr, M, C, eps, momentum, mean, rstd, run_mean, run_var, updates,
+                     num_batches_tracked);
   SM_CHECK_LAUNCH();
   return 0;
 }

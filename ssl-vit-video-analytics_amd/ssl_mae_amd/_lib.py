@@ -51,20 +51,27 @@ _SIGS = {
     "sm_gelu_fwd": (_c_i32, [_c_i32, _c_i64, _c_i32, _c_p, _c_p, _c_f32, _c_u64, _c_p]),
     "sm_colsum_workspace_bytes": (_c_i64, [_c_i64, _c_i32]),
     "sm_colsum": (_c_i32, [_c_i32, _c_i64, _c_i32, _c_p, _c_p, _c_i32, _c_p, _c_i64, _c_p]),
-    "sm_se_scale": (_c_i32, [_c_i32, _c_p, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p]),
     "sm_stem_im2col": (_c_i32, [_c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_i64, _c_i64, _c_i64, _c_i64,
                                 _c_i64, _c_i32, _c_p, _c_p]),
     "sm_im2col3": (_c_i32, [_c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p]),
     "sm_col2im3": (_c_i32, [_c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p]),
     "sm_conv_wpack": (_c_i32, [_c_i32, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p]),
     "sm_conv_wunpack_add": (_c_i32, [_c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p]),
+    "sm_se_workspace_bytes": (_c_i64, [_c_i32, _c_i32, _c_i32]),
+    "sm_se_fwd": (_c_i32, [_c_i32, _c_p] + [_c_p] * 4 + [_c_i32] * 5 + [_c_p] * 7 + [_c_i64, _c_p]),
+    "sm_se_bwd": (_c_i32, [_c_i32, _c_p, _c_p] + [_c_p] * 4 + [_c_i32] * 5 + [_c_p] * 8 + [_c_i64, _c_p]),
+    "sm_se_scale": (_c_i32, [_c_i32, _c_p] + [_c_p] * 4 + [_c_i32, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p]),
+    "sm_dwconv_fused_partial_rows": (_c_i64, [_c_i32, _c_i32, _c_i32]),
+    "sm_dwconv_fused_fwd": (_c_i32, [_c_i32] * 5 + [_c_p] * 5 + [_c_i32] + [_c_p] * 4),
+    "sm_dwconv_fused_bwd_workspace_bytes": (_c_i64, [_c_i32] * 5),
+    "sm_dwconv_fused_bwd": (_c_i32, [_c_i32] * 5 + [_c_p] * 6 + [_c_i32] + [_c_p] * 4 + [_c_i64, _c_p]),
+    "sm_bn_partials_workspace_bytes": (_c_i64, [_c_i32]),
+    "sm_bn_stats_from_partials": (_c_i32, [_c_p, _c_i64, _c_i32, _c_i64] + [_c_p] * 5 + [_c_f32, _c_f32, _c_i32,
+                                                                                       _c_p, _c_i64, _c_p]),
     "sm_dwconv_fwd": (_c_i32, [_c_i32, _c_p, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_p]),
     "sm_dwconv_wgrad_workspace_bytes": (_c_i64, [_c_i32, _c_i32, _c_i32, _c_i32, _c_i32]),
     "sm_dwconv_bwd": (_c_i32, [_c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_p,
                                _c_i64, _c_p]),
-    "sm_se_fwd": (_c_i32, [_c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
-    "sm_se_bwd": (_c_i32, [_c_i32, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p,
-                           _c_p, _c_p, _c_p, _c_p]),
     "sm_tube_mask": (_c_i32, [_c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p]),
     "sm_pos_blend_fwd": (_c_i32, [_c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_i32, _c_i32,
                                   _c_i32, _c_p]),

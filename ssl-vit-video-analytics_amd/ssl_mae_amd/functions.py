@@ -140,13 +140,24 @@ class MBConvFn(torch.autograd.Function):
         mid, Cout, s = st.mid, st.cout, st.stride
         x2d = x.reshape(-1, Cin)
         a1 = K.linear(x2d, W(w_exp, mode).view(mid, Cin))
-        h1, m0, r0 = _bn_forward(a1, st.bn0, gelu=True)
-        a2 = K.dwconv(h1, w_dw.detach().view(mid, 9), Fr, H, Wd, mid, s)
-        del h1
         Ho, Wo = (H - 1) // s + 1, (Wd - 1) // s + 1
-        h2, m2, r2 = _bn_forward(a2, st.bn2, gelu=True)
-        h3, pooled, h1se, gate = K.se_fwd(h2, Fr, Ho * Wo, mid, w_fc0.detach(), w_fc2.detach())
-        del h2
+        fused = mode.bf16 and mid % 32 == 0
+        if fused:
+            # BN0 + GELU folded into the depthwise conv's loads, BN2 statistics produced
+            # by it, BN2 + GELU folded into the SE reads: no act(a1) / act(a2) in HBM
+            m0, r0 = K.bn_stats(a1, st.bn0.running_mean, st.bn0.running_var, st.bn0.momentum, st.bn0.eps, 1,
+                                st.bn0.num_batches_tracked)
+            act0 = (m0, r0, g0.detach(), b0.detach(), True)
+            a2, m2, r2 = K.dwconv_fused(a1, act0, w_dw.detach().view(mid, 9), Fr, H, Wd, mid, s, bn_out=st.bn2)
+            act2 = (m2, r2, g2.detach(), b2.detach(), True)
+            h3, pooled, h1se, gate = K.se_fwd(a2, Fr, Ho * Wo, mid, w_fc0.detach(), w_fc2.detach(), act=act2)
+        else:
+            h1, m0, r0 = _bn_forward(a1, st.bn0, gelu=True)
+            a2 = K.dwconv(h1, w_dw.detach().view(mid, 9), Fr, H, Wd, mid, s)
+            del h1
+            h2, m2, r2 = _bn_forward(a2, st.bn2, gelu=True)
+            h3, pooled, h1se, gate = K.se_fwd(h2, Fr, Ho * Wo, mid, w_fc0.detach(), w_fc2.detach())
+            del h2
         a3 = K.linear(h3, W(w_proj, mode).view(Cout, mid))
         del h3
         mean5, rstd5 = K.bn_stats(a3, st.bn5.running_mean, st.bn5.running_var, st.bn5.momentum, st.bn5.eps, 1,
@@ -154,6 +165,7 @@ class MBConvFn(torch.autograd.Function):
         out = K.bn_apply(a3, mean5, rstd5, g5.detach(), b5.detach(), residual=x2d if st.res else None,
                          row_scale=st.dp_scale, rows_per_group=Ho * Wo)
         m5, r5 = mean5, rstd5
+        ctx.fused = fused
         ctx.st = st
         ctx.geom = (Fr, H, Wd, Cin, Ho, Wo)
         ctx.params = (w_exp, g0, b0, w_dw, g2, b2, w_fc0, w_fc2, w_proj, g5, b5)
@@ -172,22 +184,36 @@ class MBConvFn(torch.autograd.Function):
         dout2d = dout.reshape(-1, Cout).to(mode.act).contiguous()
         da3 = K.bn_bwd(dout2d, a3, m5, r5, g5.detach(), b5.detach(), False, G(g5), G(b5),
                        row_scale=st.dp_scale, rows_per_group=Ho * Wo)
-        h2 = K.bn_apply(a2, m2, r2, g2.detach(), b2.detach(), gelu=True)
-        h3 = K.se_scale(h2, gate, Fr, Ho * Wo, mid)
+        if ctx.fused:
+            act2 = (m2, r2, g2.detach(), b2.detach(), True)
+            h3 = K.se_scale(a2, gate, Fr, Ho * Wo, mid, act=act2)
+        else:
+            h2 = K.bn_apply(a2, m2, r2, g2.detach(), b2.detach(), gelu=True)
+            h3 = K.se_scale(h2, gate, Fr, Ho * Wo, mid)
         K.linear_dw(da3, h3, G(w_proj).view(Cout, mid))
         del h3
         dh3 = K.linear_dx(da3, W(w_proj, mode).view(Cout, mid))
         del da3
-        dh2, dz2, dz1 = K.se_bwd(dh3, h2, Fr, Ho * Wo, mid, w_fc0.detach(), w_fc2.detach(), gate, h1se)
-        del dh3, h2
+        if ctx.fused:
+            dh2, dz2, dz1 = K.se_bwd(dh3, a2, Fr, Ho * Wo, mid, w_fc0.detach(), w_fc2.detach(), gate, h1se, act=act2)
+        else:
+            dh2, dz2, dz1 = K.se_bwd(dh3, h2, Fr, Ho * Wo, mid, w_fc0.detach(), w_fc2.detach(), gate, h1se)
+            del h2
+        del dh3
         R = mid // 4
         K.gemm(dz2, h1se, G(w_fc2), mid, R, Fr, 1, 1, mid, R, R, beta=1.0)
         K.gemm(dz1, pooled, G(w_fc0), R, mid, Fr, 1, 1, R, mid, mid, beta=1.0)
         da2 = K.bn_bwd(dh2, a2, m2, r2, g2.detach(), b2.detach(), True, G(g2), G(b2))
         del dh2
-        h1 = K.bn_apply(a1, m0, r0, g0.detach(), b0.detach(), gelu=True)
-        dh1 = K.dwconv_bwd(da2, h1, w_dw.detach().view(mid, 9), G(w_dw).view(mid, 9), Fr, H, Wd, mid, s)
-        del h1, da2
+        if ctx.fused:
+            act0 = (m0, r0, g0.detach(), b0.detach(), True)
+            dh1 = K.dwconv_fused_bwd(da2, a1, act0, w_dw.detach().view(mid, 9), G(w_dw).view(mid, 9), Fr, H, Wd,
+                                     mid, s)
+        else:
+            h1 = K.bn_apply(a1, m0, r0, g0.detach(), b0.detach(), gelu=True)
+            dh1 = K.dwconv_bwd(da2, h1, w_dw.detach().view(mid, 9), G(w_dw).view(mid, 9), Fr, H, Wd, mid, s)
+            del h1
+        del da2
         da1 = K.bn_bwd(dh1, a1, m0, r0, g0.detach(), b0.detach(), True, G(g0), G(b0))
         del dh1
         x2d = x.reshape(-1, Cin)

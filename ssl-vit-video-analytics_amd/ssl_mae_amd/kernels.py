@@ -260,33 +260,83 @@ def dwconv_bwd(dy, x, w, dw_sink, F, H, W, C, stride, need_dx=True):
     return dx
 
 
-def se_fwd(x, F, HW, C, w1, w2):
+def _act_args(act):
+    """act = None or (mean, rstd, weight, bias, gelu): the BN(+GELU) folded into loads."""
+    if act is None:
+        return [None, None, None, None, 0]
+    mean, rstd, w, b, gelu = act
+    return [ptr(mean), ptr(rstd), ptr(w), ptr(b), 1 if gelu else 0]
+
+
+def dwconv_fused(x, act, w, F, H, W, C, stride, bn_out=None):
+    """y = dwconv3x3(act(x)) (bf16); with bn_out (a BatchNorm2d module) also its
+    train-mode statistics of y: returns (y, mean, rstd) (or y)."""
+    _chk(x)
+    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    dev = x.device
+    y = torch.empty((F * Ho * Wo, C), dtype=x.dtype, device=dev)
+    part = None
+    if bn_out is not None:
+        rows = query("sm_dwconv_fused_partial_rows", F, H, stride)
+        part = torch.empty((rows, 2, C), dtype=torch.float32, device=dev)
+    a = _act_args(act)
+    call("sm_dwconv_fused_fwd", F, H, W, C, stride, ptr(x), a[0], a[1], a[2], a[3], a[4], ptr(w), ptr(y), ptr(part),
+         stream())
+    if bn_out is None:
+        return y
+    mean = torch.empty(C, dtype=torch.float32, device=dev)
+    rstd = torch.empty(C, dtype=torch.float32, device=dev)
+    nbytes = query("sm_bn_partials_workspace_bytes", C)
+    ws = _ws(nbytes, dev)
+    call("sm_bn_stats_from_partials", ptr(part), part.shape[0], C, F * Ho * Wo, ptr(mean), ptr(rstd),
+         ptr(bn_out.running_mean), ptr(bn_out.running_var), ptr(bn_out.num_batches_tracked),
+         float(bn_out.momentum), float(bn_out.eps), 1, ptr(ws), nbytes, stream())
+    return y, mean, rstd
+
+
+def dwconv_fused_bwd(dy, x, act, w, dw_sink, F, H, W, C, stride, need_dx=True):
+    """dx = dL/d act(x), dw_sink += dL/dw for y = dwconv3x3(act(x)) (bf16)."""
+    _chk(dy, x)
+    dx = torch.empty_like(x) if need_dx else None
+    nbytes = query("sm_dwconv_fused_bwd_workspace_bytes", F, H, W, C, stride)
+    ws = _ws(nbytes, x.device)
+    a = _act_args(act)
+    call("sm_dwconv_fused_bwd", F, H, W, C, stride, ptr(dy), ptr(x), a[0], a[1], a[2], a[3], a[4], ptr(w), ptr(dx),
+         ptr(dw_sink), ptr(ws), nbytes, stream())
+    return dx
+
+
+def se_fwd(x, F, HW, C, w1, w2, act=None, want_y=True):
+    """SELayer on h = act(x): returns (y = h * gate, pooled, relu(z1), gate)."""
     R = w1.shape[0]
     dev = x.device
     pooled = torch.empty((F, C), dtype=torch.float32, device=dev)
     h1 = torch.empty((F, R), dtype=torch.float32, device=dev)
     s = torch.empty((F, C), dtype=torch.float32, device=dev)
-    y = torch.empty_like(x)
-    call("sm_se_fwd", dt(x), ptr(x), F, HW, C, R, ptr(w1), ptr(w2), ptr(pooled), ptr(h1), ptr(s), ptr(y), stream())
+    y = torch.empty_like(x) if want_y else None
+    nbytes = query("sm_se_workspace_bytes", F, HW, C)
+    ws = _ws(nbytes, dev)
+    call("sm_se_fwd", dt(x), ptr(x), *_act_args(act), F, HW, C, R, ptr(w1), ptr(w2), ptr(pooled), ptr(h1), ptr(s),
+         ptr(y), ptr(ws), nbytes, stream())
     return y, pooled, h1, s
 
 
-def se_scale(x, s, F, HW, C):
+def se_scale(x, s, F, HW, C, act=None):
     y = torch.empty_like(x)
-    call("sm_se_scale", dt(x), ptr(x), ptr(s), ptr(y), F, HW, C, stream())
+    call("sm_se_scale", dt(x), ptr(x), *_act_args(act), ptr(s), ptr(y), F, HW, C, stream())
     return y
 
 
-def se_bwd(dy, x, F, HW, C, w1, w2, s, h1):
+def se_bwd(dy, x, F, HW, C, w1, w2, s, h1, act=None):
     R = w1.shape[0]
     dev = x.device
-    ds = torch.empty((F, C), dtype=torch.float32, device=dev)
     dz2 = torch.empty((F, C), dtype=torch.float32, device=dev)
     dz1 = torch.empty((F, R), dtype=torch.float32, device=dev)
-    dpool = torch.empty((F, C), dtype=torch.float32, device=dev)
     dx = torch.empty_like(x)
-    call("sm_se_bwd", dt(x), ptr(dy), ptr(x), F, HW, C, R, ptr(w1), ptr(w2), ptr(s), ptr(h1), ptr(ds), ptr(dz2),
-         ptr(dz1), ptr(dpool), ptr(dx), stream())
+    nbytes = query("sm_se_workspace_bytes", F, HW, C)
+    ws = _ws(nbytes, dev)
+    call("sm_se_bwd", dt(x), ptr(dy), ptr(x), *_act_args(act), F, HW, C, R, ptr(w1), ptr(w2), ptr(s), ptr(h1),
+         ptr(dz2), ptr(dz1), ptr(dx), ptr(ws), nbytes, stream())
     return dx, dz2, dz1
 
 

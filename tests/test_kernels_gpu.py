@@ -336,6 +336,74 @@ def test_se_layer(dtype):
     assert rel_err(dw1, w1r.grad) < (1e-4 if dtype == torch.float32 else 2e-2)
 
 
+# ------------------------------------------------------------------ fused MBConv depthwise / SE paths
+class _BN:
+    def __init__(self, C):
+        self.running_mean = torch.zeros(C, device=DEV)
+        self.running_var = torch.ones(C, device=DEV)
+        self.num_batches_tracked = torch.zeros((), dtype=torch.int64, device=DEV)
+        self.momentum, self.eps = 0.1, 1e-5
+
+
+def _act_for(a2d, seed):
+    """BN(train) + GELU parameters of a [M][C] pre-activation (the MBConv producer)."""
+    kk = KK()
+    C = a2d.shape[1]
+    g = (rnd(C, seed=seed) * 0.2 + 1).to(DEV)
+    b = (rnd(C, seed=seed + 1) * 0.2).to(DEV)
+    m, r = kk.bn_stats(a2d)
+    return (m, r, g, b, True)
+
+
+@pytest.mark.parametrize("stride,H,W,C", [(1, 14, 14, 64), (1, 9, 23, 32), (2, 14, 14, 64), (2, 13, 11, 96)])
+def test_dwconv_fused_matches_unfused(stride, H, W, C):
+    """dwconv(act(x)) with act folded into the loads == bn_apply + dwconv (bit-exact y);
+    in-kernel BN statistics == a separate bn_stats pass; backward (dx, dw) == the
+    unfused backward on the materialised act(x)."""
+    kk = KK()
+    Fn = 3
+    a = (rnd(Fn * H * W, C, seed=90) * 2 + 0.5).to(torch.bfloat16).to(DEV)
+    w = (rnd(C, 9, seed=91) * 0.3).to(DEV)
+    act = _act_for(a, 92)
+    h = kk.bn_apply(a, act[0], act[1], act[2], act[3], gelu=True)
+    y_ref = kk.dwconv(h, w, Fn, H, W, C, stride)
+    bn_f, bn_r = _BN(C), _BN(C)
+    y, mean, rstd = kk.dwconv_fused(a, act, w, Fn, H, W, C, stride, bn_out=bn_f)
+    assert torch.equal(y, y_ref)
+    m_ref, r_ref = kk.bn_stats(y_ref, bn_r.running_mean, bn_r.running_var, 0.1, 1e-5, 1, bn_r.num_batches_tracked)
+    assert rel_err(mean, m_ref) < 1e-5 and rel_err(rstd, r_ref) < 1e-5
+    assert rel_err(bn_f.running_var, bn_r.running_var) < 1e-5 and int(bn_f.num_batches_tracked) == 1
+    dy = rnd(*y.shape, seed=93).to(torch.bfloat16).to(DEV)
+    dw_ref = torch.zeros(C, 9, device=DEV)
+    dx_ref = kk.dwconv_bwd(dy, h, w, dw_ref, Fn, H, W, C, stride)
+    dw = torch.zeros(C, 9, device=DEV)
+    dx = kk.dwconv_fused_bwd(dy, a, act, w, dw, Fn, H, W, C, stride)
+    assert rel_err(dx, dx_ref) < 1e-2
+    assert rel_err(dw, dw_ref) < 1e-4
+
+
+@pytest.mark.parametrize("HW,C", [(49, 96), (900, 64), (1600, 384)])
+def test_se_fused_act_matches_materialised(HW, C):
+    """SE on act(x) recomputed in its kernels == SE on the materialised act(x)."""
+    kk = KK()
+    Fn, R = 3, C // 4
+    a = (rnd(Fn * HW, C, seed=95) * 2).to(torch.bfloat16).to(DEV)
+    act = _act_for(a, 96)
+    h = kk.bn_apply(a, act[0], act[1], act[2], act[3], gelu=True)
+    w1 = (rnd(R, C, seed=97) * 0.2).to(DEV)
+    w2 = (rnd(C, R, seed=98) * 0.2).to(DEV)
+    y_r, p_r, h1_r, s_r = kk.se_fwd(h, Fn, HW, C, w1, w2)
+    y, p, h1, s = kk.se_fwd(a, Fn, HW, C, w1, w2, act=act)
+    assert rel_err(p, p_r) < 1e-5 and rel_err(s, s_r) < 1e-5
+    assert rel_err(y, y_r) < 1e-2
+    assert torch.equal(kk.se_scale(a, s, Fn, HW, C, act=act), kk.se_scale(h, s, Fn, HW, C))
+    dy = rnd(Fn * HW, C, seed=99).to(torch.bfloat16).to(DEV)
+    dx_r, dz2_r, dz1_r = kk.se_bwd(dy, h, Fn, HW, C, w1, w2, s, h1)
+    dx, dz2, dz1 = kk.se_bwd(dy, a, Fn, HW, C, w1, w2, s, h1, act=act)
+    assert rel_err(dz2, dz2_r) < 1e-5 and rel_err(dz1, dz1_r) < 1e-5
+    assert rel_err(dx, dx_r) < 1e-2
+
+
 # ------------------------------------------------------------------ MAE glue
 def test_tube_mask_and_gather_bit_exact():
     from oracle import mae_oracle as O
