@@ -72,6 +72,30 @@ def cpu_baseline(T, S, ratio):
                       f"(dropout off) on {threads} host threads; {dt:.1f} s"}
 
 
+PROBE_KERNELS = {"dec_attn_fwd": "attn_fwd_bf16<64, true>"}
+
+
+def pmc_traffic(probe, B, T, S):
+    """HBM bytes per launch of the probe kernel, measured with PMC counters by
+    scripts/pmc_traffic.sh (FETCH_SIZE / WRITE_SIZE passes over this bench at the
+    default workload) and committed as profiles/*_traffic.json; None if absent."""
+    import glob
+    if (B, T, S) != (256, 8, 224):
+        return None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("kernel") == PROBE_KERNELS.get(probe):
+            L = T * (S // 8) ** 2
+            algo = B * L * (3 * 384 + 384) * 2 + B * 6 * L * 4    # qkv read + O write (bf16) + lse
+            return {"traffic": round(d["traffic_bytes"] / 1e9, 3), "traffic_unit": "GB/launch",
+                    "algorithmic_gb_per_launch": round(algo / 1e9, 3),
+                    "traffic_source": os.path.relpath(f, ROOT)}
+    return None
+
+
 class Probe:
     """HIP-event timing of one kernel group on the stream it is launched on."""
 
@@ -194,6 +218,9 @@ def main():
                     "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None,
                     "avg_launch_ms": round(avg, 3), "launches": len(probe.pairs),
                     "algorithmic_flop_per_launch": flop_per_launch}
+            tr = pmc_traffic(args.probe, B, T, S)
+            if tr:
+                roof.update(tr)
         step_tflops = value / world * TRAIN_TFLOP_PER_CLIP
         cpu = None
         if not args.no_cpu_baseline and world == 1:

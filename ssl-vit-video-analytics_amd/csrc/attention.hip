@@ -58,6 +58,32 @@ SM_DEV int tile_off(int row, int d) {
   (void)CPR;
 }
 
+// combine a value with the lane 32 apart (the other half-wave) by v_permlane32_swap
+// (no LDS round trip): the two results hold {own, other} in either order
+SM_DEV float halves_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+SM_DEV float halves_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// 1-D grid over (query/key block, head, sample) with the bijective XCD remap: all
+// blocks of one (sample, head) run on the same XCD, so the K/V (or Q/dO) panel they
+// all stream is fetched into that XCD's L2 once instead of once per XCD.
+struct AttnTile {
+  int qb, hd, n;
+  SM_DEV AttnTile(int nqb, int H) {
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    qb = v % nqb;
+    hd = (v / nqb) % H;
+    n = v / (nqb * H);
+  }
+};
+
 // accumulator (32x32) -> bf16 B-operand fragment for k-step s
 SM_DEV bf16x8 acc_to_frag(const f32x16& a, int s) {
   bf16x8 f;
@@ -132,7 +158,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(AttnArgs a) {
   constexpr int RB = 32 * D * 2;   // bytes of 32 tile rows
   __shared__ __attribute__((aligned(16))) char lk[KT * D * 2];
   __shared__ __attribute__((aligned(16))) char lv[KT * D * 2];
-  const int n = blockIdx.z, hd = blockIdx.y;
+  const AttnTile tl((a.L + 127) / 128, a.H);
+  const int n = tl.n, hd = tl.hd;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5;
   const int C = a.H * D;
   const int ldq = 3 * C;
@@ -140,7 +167,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(AttnArgs a) {
   const __bf16* qb = qkv + hd * D;
   const __bf16* kb = qkv + C + hd * D;
   const __bf16* vb = qkv + 2 * C + hd * D;
-  const int q = blockIdx.x * 128 + w * 32 + (l & 31);
+  const int q = tl.qb * 128 + w * 32 + (l & 31);
 
   bf16x8 qf[D / 16];
 #pragma unroll
@@ -200,7 +227,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(AttnArgs a) {
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int r = 0; r < 16; ++r) mt = fmaxf(mt, st[u][r]);
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * c;
+    mt = halves_max(mt) * c;
     // rescale only when some row's max grew (exact: alpha == 1 otherwise)
     const bool grow = mt > m;
     const float mn = grow ? mt : m;
@@ -240,7 +267,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(AttnArgs a) {
               lds_tr(lv, vlo[t] + u * RB + s * (RB / 2), vhi[t] + u * RB + s * (RB / 2)), pf, o[t], 0, 0, 0);
       }
   }
-  lsum += __shfl_xor(lsum, 32, 64);
+  lsum = halves_sum(lsum);
   if (q < a.L) {
     const float inv = (DROP ? 1.f / (1.f - a.drop_p) : 1.f) / lsum;
     __bf16* ob = (__bf16*)a.out + ((int64_t)n * a.L + q) * C + hd * D;
@@ -287,7 +314,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char ldo[QT * D * 2];
   __shared__ __attribute__((aligned(16))) float llse[QT];
   __shared__ __attribute__((aligned(16))) float ldel[QT];
-  const int n = blockIdx.z, hd = blockIdx.y;
+  const AttnTile tl((a.L + 127) / 128, a.H);
+  const int n = tl.n, hd = tl.hd;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5;
   const int C = a.H * D;
   const int ldq = 3 * C;
@@ -298,7 +326,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(AttnArgs a) {
   const __bf16* dob = (const __bf16*)a.dout + (int64_t)n * a.L * C + hd * D;
   const float* lse = a.lse + ((int64_t)n * a.H + hd) * a.L;
   const float* del = a.delta + ((int64_t)n * a.H + hd) * a.L;
-  const int key = blockIdx.x * 128 + w * 32 + (l & 31);
+  const int key = tl.qb * 128 + w * 32 + (l & 31);
 
   bf16x8 kf[D / 16], vf[D / 16];
 #pragma unroll
@@ -434,7 +462,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16(AttnArgs a) {
   constexpr int RB = 32 * D * 2;
   __shared__ __attribute__((aligned(16))) char lk[KT * D * 2];
   __shared__ __attribute__((aligned(16))) char lv[KT * D * 2];
-  const int n = blockIdx.z, hd = blockIdx.y;
+  const AttnTile tl((a.L + 127) / 128, a.H);
+  const int n = tl.n, hd = tl.hd;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5;
   const int C = a.H * D;
   const int ldq = 3 * C;
@@ -443,7 +472,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16(AttnArgs a) {
   const __bf16* kb = qkv + C + hd * D;
   const __bf16* vb = qkv + 2 * C + hd * D;
   const __bf16* dob = (const __bf16*)a.dout + (int64_t)n * a.L * C + hd * D;
-  const int q = blockIdx.x * 128 + w * 32 + (l & 31);
+  const int q = tl.qb * 128 + w * 32 + (l & 31);
   const bool qok = q < a.L;
   const float lse2 = qok ? a.lse[((int64_t)n * a.H + hd) * a.L + q] * LOG2E : 1e30f;
   const float dl = qok ? a.delta[((int64_t)n * a.H + hd) * a.L + q] : 0.f;
@@ -681,14 +710,15 @@ extern "C" int sm_attn_fwd(int dtype, int N, int L, int H, int D, const void* qk
   a.qkv = qkv; a.out = out; a.lse = lse; a.N = N; a.L = L; a.H = H; a.scale = scale;
   a.drop_p = drop_p; a.seed = seed;
   dim3 grid((L + 127) / 128, H, N);
+  const dim3 grid1((unsigned)(((L + 127) / 128) * H * N));   // bf16 kernels: 1-D, XCD-remapped
   const bool drop = drop_p > 0.f;
   if (dtype == SM_BF16) {
     if (D == 32) {
-      if (drop) hipLaunchKernelGGL((attn_fwd_bf16<32, true>), grid, dim3(256), 0, st, a);
-      else hipLaunchKernelGGL((attn_fwd_bf16<32, false>), grid, dim3(256), 0, st, a);
+      if (drop) hipLaunchKernelGGL((attn_fwd_bf16<32, true>), grid1, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((attn_fwd_bf16<32, false>), grid1, dim3(256), 0, st, a);
     } else {
-      if (drop) hipLaunchKernelGGL((attn_fwd_bf16<64, true>), grid, dim3(256), 0, st, a);
-      else hipLaunchKernelGGL((attn_fwd_bf16<64, false>), grid, dim3(256), 0, st, a);
+      if (drop) hipLaunchKernelGGL((attn_fwd_bf16<64, true>), grid1, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((attn_fwd_bf16<64, false>), grid1, dim3(256), 0, st, a);
     }
   } else {
     if (D == 32) hipLaunchKernelGGL(attn_fwd_f32<32>, grid, dim3(128), 0, st, a);
@@ -712,11 +742,12 @@ extern "C" int sm_attn_bwd(int dtype, int N, int L, int H, int D, const void* qk
   else hipLaunchKernelGGL(attn_delta_kernel<float>, dim3(dblocks), dim3(256), 0, st, a, D);
   SM_CHECK_LAUNCH();
   dim3 grid((L + 127) / 128, H, N);
+  const dim3 grid1((unsigned)(((L + 127) / 128) * H * N));   // bf16 kernels: 1-D, XCD-remapped
   const bool drop = drop_p > 0.f;
   if (dtype == SM_BF16) {
 #define SM_ATTN_BWD(DD, DR)                                                        \
-  hipLaunchKernelGGL((attn_bwd_dkdv_bf16<DD, DR>), grid, dim3(256), 0, st, a);    \
-  hipLaunchKernelGGL((attn_bwd_dq_bf16<DD, DR>), grid, dim3(256), 0, st, a);
+  hipLaunchKernelGGL((attn_bwd_dkdv_bf16<DD, DR>), grid1, dim3(256), 0, st, a);    \
+  hipLaunchKernelGGL((attn_bwd_dq_bf16<DD, DR>), grid1, dim3(256), 0, st, a);
     if (D == 32) { if (drop) { SM_ATTN_BWD(32, true) } else { SM_ATTN_BWD(32, false) } }
     else { if (drop) { SM_ATTN_BWD(64, true) } else { SM_ATTN_BWD(64, false) } }
 #undef SM_ATTN_BWD
