@@ -93,10 +93,64 @@ SM_DEV bf16x8 acc_to_frag(const f32x16& a, int s) {
 }
 SM_DEV int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
-// dropout keep multiplier for P[n,hd,q,k] (f32 kernels): row (n*H+hd)*L+q, column k
+// ---------- attention-probability dropout mask ------------------------------------
+// keep(row, col), row = (n*H + hd)*L + q, col = key:
+//   h    = mix24(seed32 + row * AG + (col >> 2) * AC)     one hash per 4 keys
+//   keep = (byte (col & 3) of h) & 0x7F >= round(128 p)   (p = 0.1: 13/128 dropped)
+// common.h's fmix32 input, but mixed with 24-bit multiplies (v_mul_u32_u24, full
+// rate) instead of fmix32's 32-bit ones (v_mul_lo_u32, quarter rate): these kernels
+// are bound by VALU issue, and the hash was the largest item in it.  Every term
+// that varies along a kernel's tile loop is wave-uniform (scalar ALU), so a hash
+// costs one vector add plus the 6-op mix.  (Keep rate, row/column balance and
+// neighbour correlations measured equal to fmix32's on 4096 x 4096 masks.)
+constexpr uint32_t AG = 0x9E3779B1u;   // row multiplier
+constexpr uint32_t AC = 0x7FEB352Du;   // column-group multiplier
+SM_DEV uint32_t mix24(uint32_t x) {
+  x ^= x >> 16;
+  x = (x & 0xFFFFFFu) * 0xEBCA6Bu;
+  x ^= x >> 13;
+  x = (x & 0xFFFFFFu) * 0xB2AE35u;
+  x ^= x >> 16;
+  return x;
+}
+SM_DEV uint32_t attn_keep_hash(uint32_t s32, uint64_t row, uint32_t col) {
+  return mix24(s32 + (uint32_t)row * AG + (col >> 2) * AC);
+}
+SM_DEV uint32_t attn_thr(float p) { return (uint32_t)(p * 128.f + 0.5f); }
+SM_DEV bool attn_keep_byte(uint32_t h, int j, uint32_t thr) { return ((h >> (8 * j)) & 0x7Fu) >= thr; }
+
+// Packed form for bf16 P pairs: bit 7 of byte j of keep_flags() is keep(j) (7-bit
+// SWAR compare: (b & 0x7F) + 128 - thr never carries out of its byte), and v_perm's
+// sign-replicating selectors (8/9: bit 15/31 of the second source, 10/11: of the
+// first) expand two flags into a 16-bit-per-element mask in one instruction.
+SM_DEV uint32_t keep_flags(uint32_t h, uint32_t thr) { return (h & 0x7F7F7F7Fu) + (128u - thr) * 0x01010101u; }
+SM_DEV uint32_t keep_mask01(uint32_t y) { return __builtin_amdgcn_perm(y << 8, y, 0x08080A0Au); }   // bytes 0, 1
+SM_DEV uint32_t keep_mask23(uint32_t y) { return __builtin_amdgcn_perm(y << 8, y, 0x09090B0Bu); }   // bytes 2, 3
+SM_DEV uint32_t pack_bf16x2(float lo, float hi) {
+  typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+  const bf16x2 v = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(uint32_t, v);
+}
+
+// dropout keep multiplier for P[n,hd,q,k] (f32 kernels)
 SM_DEV float drop_keep_scale(const AttnArgs& a, int n, int hd, int q, int k) {
   const uint64_t row = (uint64_t)(n * a.H + hd) * a.L + q;
-  return drop_keep(seed32(a.seed), row, (uint32_t)k, drop_thr(a.drop_p)) ? 1.0f / (1.0f - a.drop_p) : 0.0f;
+  const uint32_t h = attn_keep_hash(seed32(a.seed), row, (uint32_t)k);
+  return attn_keep_byte(h, k & 3, attn_thr(a.drop_p)) ? 1.0f / (1.0f - a.drop_p) : 0.0f;
+}
+
+// 4x4 byte transpose inside a DPP quad: lane i's byte j <- lane j's byte i.  Stage 1
+// swaps 16-bit halves with lane i^2, stage 2 bytes with lane i^1 (v_perm selectors
+// per lane from quad_sel()).
+SM_DEV void quad_sel(int kq, uint32_t& sel1, uint32_t& sel2) {
+  sel1 = (kq & 2) ? 0x03020706u : 0x05040100u;
+  sel2 = (kq & 1) ? 0x03070105u : 0x06020400u;
+}
+SM_DEV uint32_t quad_transpose_bytes(uint32_t v, uint32_t sel1, uint32_t sel2) {
+  const uint32_t p = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);   // lane ^ 2
+  v = __builtin_amdgcn_perm(p, v, sel1);
+  const uint32_t q = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // lane ^ 1
+  return __builtin_amdgcn_perm(q, v, sel2);
 }
 
 // Per-thread plan for staging a [ROWS][D] bf16 tile (rows of a [L][ld] matrix) into
@@ -190,8 +244,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(AttnArgs a) {
     for (int r = 0; r < 16; ++r) o[t][r] = 0.f;
   float m = NEG_BIG, lsum = 0.f;
   const float c = a.scale * LOG2E;
-  const uint32_t drb = drop_rowbase(seed32(a.seed), (uint64_t)(n * a.H + hd) * a.L + q);
-  const uint32_t dthr = drop_thr(a.drop_p);
+  // hash input minus its wave-uniform column part: row term + this half's group
+  const uint32_t dlb = seed32(a.seed) + (uint32_t)((uint64_t)(n * a.H + hd) * a.L + q) * AG + (uint32_t)h * AC;
+  const uint32_t dthr = attn_thr(a.drop_p);
 
   uint4 rk[Stager<D, KT>::CH], rv[Stager<D, KT>::CH];
   stg.load(kb, a.L, rk);
@@ -234,19 +289,25 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(AttnArgs a) {
     const float alpha = grow ? __builtin_amdgcn_exp2f(m - mn) : 1.f;
     m = mn;
     float ps = 0.f;
+    uint32_t pw[2][4][2];   // bf16 pairs of P (dropout applied): [u][g][keys 4g+0,1 | 4g+2,3]
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        uint32_t hv = 0;
-        if (DROP) hv = drop_hash(drb, (uint32_t)(k0 + 32 * u + 8 * g + 4 * h));   // keys 4g'..+3 share it
+        float p4[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int r = 4 * g + j;
-          const float p = __builtin_amdgcn_exp2f(fmaf(st[u][r], c, -mn));
-          ps += p;
-          st[u][r] = (!DROP || ((hv >> (8 * j)) & 0xFFu) >= dthr) ? p : 0.f;
+          p4[j] = __builtin_amdgcn_exp2f(fmaf(st[u][4 * g + j], c, -mn));
+          ps += p4[j];
         }
+        uint32_t w0 = pack_bf16x2(p4[0], p4[1]), w1 = pack_bf16x2(p4[2], p4[3]);
+        if (DROP) {   // keys k0+32u+8g+4h+j, j = 0..3, share one hash; masks on the packed pairs
+          const uint32_t y = keep_flags(mix24(dlb + (uint32_t)((k0 >> 2) + 8 * u + 2 * g) * AC), dthr);
+          w0 &= keep_mask01(y);
+          w1 &= keep_mask23(y);
+        }
+        pw[u][g][0] = w0;
+        pw[u][g][1] = w1;
       }
     }
     lsum = lsum * alpha + ps;
@@ -260,7 +321,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(AttnArgs a) {
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const bf16x8 pf = acc_to_frag(st[u], s);
+        const bf16x8 pf = __builtin_bit_cast(
+            bf16x8, make_uint4(pw[u][2 * s][0], pw[u][2 * s][1], pw[u][2 * s + 1][0], pw[u][2 * s + 1][1]));
 #pragma unroll
         for (int t = 0; t < D / 32; ++t)
           o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
@@ -354,9 +416,17 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(AttnArgs a) {
     for (int r = 0; r < 16; ++r) { dk[t][r] = 0.f; dv[t][r] = 0.f; }
   const float c = a.scale * LOG2E;
   const float ks = DROP ? 1.f / (1.f - a.drop_p) : 1.f;
-  const uint32_t s32 = seed32(a.seed), dthr = drop_thr(a.drop_p);
+  const uint32_t dthr = attn_thr(a.drop_p);
   const int kq = l & 3;                       // == key & 3: byte of the shared hash
-  const uint64_t row0 = (uint64_t)(n * a.H + hd) * a.L;
+  // Dropout: the hash of (query row, this key's 4-key group) covers the whole DPP
+  // quad of keys.  Lane kq hashes query row 4g + kq of each 16-row group, then a
+  // quad byte transpose hands every lane its own key's byte of all four rows.
+  // dlb = hash input of row q0 + 32u + 8g + 4h + kq minus the wave-uniform
+  // (q0 + 32u + 8g) * AG.
+  const uint32_t dlb = seed32(a.seed) + ((uint32_t)((uint64_t)(n * a.H + hd) * a.L) + 4 * h + kq) * AG +
+                       (uint32_t)(key >> 2) * AC;
+  uint32_t sel1, sel2;
+  quad_sel(kq, sel1, sel2);
 
   uint4 rq[Stager<D, QT>::CH], rd[Stager<D, QT>::CH];
   sq.load(qb, a.L, rq);
@@ -385,28 +455,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(AttnArgs a) {
         sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_b128(lq, roff[s] + u * RB), kf[s], sacc, 0, 0, 0);
         dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_b128(ldo, roff[s] + u * RB), vf[s], dpacc, 0, 0, 0);
       }
-      uint32_t km = 0xFFFFu;   // bit r: P[row r] kept for this lane's key
-      if (DROP) {
-        // one hash per (query row, 4-key group): the quad's lanes (keys 4m..4m+3)
-        // each hash the rows r = 4g + lane&3, then broadcast within the quad (DPP);
-        // each broadcast hash is reduced to this lane's keep bit at once
-        km = 0;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int qr = q0 + 32 * u + 8 * g + 4 * h + kq;        // acc_row(4g + kq, h)
-          const int mine = (int)drop_hash(drop_rowbase(s32, row0 + qr), (uint32_t)key);
-          uint32_t hv[4];
-          hv[0] = (uint32_t)__builtin_amdgcn_mov_dpp(mine, 0x00, 0xF, 0xF, false);
-          hv[1] = (uint32_t)__builtin_amdgcn_mov_dpp(mine, 0x55, 0xF, 0xF, false);
-          hv[2] = (uint32_t)__builtin_amdgcn_mov_dpp(mine, 0xAA, 0xF, 0xF, false);
-          hv[3] = (uint32_t)__builtin_amdgcn_mov_dpp(mine, 0xFF, 0xF, 0xF, false);
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            km |= (((hv[j] >> (8 * kq)) & 0xFFu) >= dthr ? 1u : 0u) << (4 * g + j);
-        }
-      }
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
+        uint32_t kb4 = 0;   // byte j: 7-bit keep byte of (query row 4g + j, this key)
+        if (DROP) kb4 = quad_transpose_bytes(mix24(dlb + (uint32_t)(q0 + 32 * u + 8 * g) * AG), sel1, sel2) & 0x7F7F7F7Fu;
         const float4 a4 = *(const float4*)&llse[32 * u + 8 * g + 4 * h];
         const float4 b4 = *(const float4*)&ldel[32 * u + 8 * g + 4 * h];
         const float lse4[4] = {a4.x, a4.y, a4.z, a4.w};
@@ -415,15 +467,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(AttnArgs a) {
         for (int j = 0; j < 4; ++j) {
           const int r = 4 * g + j;
           const float p = __builtin_amdgcn_exp2f(fmaf(sacc[r], c, -lse4[j]));
-          float dp = dpacc[r];
+          const float dp = dpacc[r];
           if (DROP) {
-            const bool keep = (km >> r) & 1u;
-            dp = keep ? dp * ks : 0.f;
-            sacc[r] = keep ? p * ks : 0.f;   // dropped P feeds dV
+            const bool keep = ((kb4 >> (8 * j)) & 0xFFu) >= dthr;
+            sacc[r] = keep ? p : 0.f;                          // dropped P feeds dV (x ks at the end)
+            dpacc[r] = p * fmaf(keep ? dp : 0.f, ks, -del4[j]);   // dS
           } else {
             sacc[r] = p;
+            dpacc[r] = p * (dp - del4[j]);
           }
-          dpacc[r] = p * (dp - del4[j]);     // dS
         }
       }
 #pragma unroll
@@ -447,7 +499,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(AttnArgs a) {
       for (int g = 0; g < 4; ++g) {
         float vk[4], vv[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) { vk[i] = dk[t][4 * g + i] * a.scale; vv[i] = dv[t][4 * g + i]; }
+        for (int i = 0; i < 4; ++i) { vk[i] = dk[t][4 * g + i] * a.scale; vv[i] = dv[t][4 * g + i] * ks; }
         store4(out + C + 32 * t + 8 * g + 4 * h, vk);
         store4(out + 2 * C + 32 * t + 8 * g + 4 * h, vv);
       }
@@ -501,8 +553,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16(AttnArgs a) {
     for (int r = 0; r < 16; ++r) dq[t][r] = 0.f;
   const float c = a.scale * LOG2E;
   const float ks = DROP ? 1.f / (1.f - a.drop_p) : 1.f;
-  const uint32_t drb = drop_rowbase(seed32(a.seed), (uint64_t)(n * a.H + hd) * a.L + q);
-  const uint32_t dthr = drop_thr(a.drop_p);
+  const uint32_t dlb = seed32(a.seed) + (uint32_t)((uint64_t)(n * a.H + hd) * a.L + q) * AG + (uint32_t)h * AC;
+  const uint32_t dthr = attn_thr(a.drop_p);
 
   uint4 rk[Stager<D, KT>::CH], rv[Stager<D, KT>::CH];
   stg.load(kb, a.L, rk);
@@ -527,18 +579,22 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16(AttnArgs a) {
         sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_b128(lk, roff[s] + u * RB), qf[s], sacc, 0, 0, 0);
         dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_b128(lv, roff[s] + u * RB), df[s], dpacc, 0, 0, 0);
       }
+      if (ragged) {   // keys past L: P = exp2(-huge) = 0 (uniform branch, last tile only)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (k0 + 32 * u + acc_row(r, h) >= a.L) sacc[r] = NEG_BIG;
+      }
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         uint32_t hv = 0;
-        if (DROP) hv = drop_hash(drb, (uint32_t)(k0 + 32 * u + 8 * g + 4 * h));
+        if (DROP) hv = mix24(dlb + (uint32_t)((k0 >> 2) + 8 * u + 2 * g) * AC) & 0x7F7F7F7Fu;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int r = 4 * g + j;
-          float p = __builtin_amdgcn_exp2f(fmaf(sacc[r], c, -lse2));
-          if (ragged && k0 + 32 * u + acc_row(r, h) >= a.L) p = 0.f;
-          float dp = dpacc[r];
-          if (DROP) dp = ((hv >> (8 * j)) & 0xFFu) >= dthr ? dp * ks : 0.f;
-          dpacc[r] = p * (dp - dl);
+          const float p = __builtin_amdgcn_exp2f(fmaf(sacc[r], c, -lse2));
+          const float dp = dpacc[r];
+          if (DROP) dpacc[r] = p * fmaf(((hv >> (8 * j)) & 0xFFu) >= dthr ? dp : 0.f, ks, -dl);
+          else dpacc[r] = p * (dp - dl);
         }
       }
 #pragma unroll

@@ -138,25 +138,33 @@ def test_attention_dropout_statistics():
     qkv = rnd(N * L, 3 * H * D, dtype=torch.bfloat16, seed=30).to(DEV)
     kk = KK()
     o0, _ = kk.attn_fwd(qkv, N, L, H, D)
-    outs = [kk.attn_fwd(qkv, N, L, H, D, drop_p=0.1, seed=s)[0].float() for s in range(64)]
+    outs = [kk.attn_fwd(qkv, N, L, H, D, drop_p=0.1, seed=s)[0].float() for s in range(256)]
     again = kk.attn_fwd(qkv, N, L, H, D, drop_p=0.1, seed=0)[0].float()
     assert torch.equal(outs[0], again)
     mean = torch.stack(outs).mean(0)
-    assert rel_err(mean, o0.float()) < 0.1
+    assert rel_err(mean, o0.float()) < 0.1   # ~0.05 expected at 256 samples
 
 
-def _np_keep(rows, cols, p, seed):
+def _np_keep(rows, cols, p, seed, attn=False):
     """numpy restatement of csrc/common.h drop_keep (counter hash, 8-bit threshold,
-    one fmix32 per 4 columns): keep[row, col] for the given index vectors."""
+    one hash per 4 columns): keep[row, col] for the given index vectors.  attn=True:
+    the attention kernels' rule (csrc/attention.hip): mix24 instead of fmix32 and a
+    7-bit threshold, (byte & 0x7F) >= round(128 p)."""
     M = 0xFFFFFFFF
     s32 = (seed & M) ^ (seed >> 32)
     r = rows.astype(np.uint64)[:, None]
     c = cols.astype(np.uint64)[None, :]
     h = (s32 + r * 0x9E3779B1 + (c >> 2) * 0x7FEB352D) & M
-    h ^= h >> 16; h = (h * 0x85EBCA6B) & M
-    h ^= h >> 13; h = (h * 0xC2B2AE35) & M
+    if attn:
+        h ^= h >> 16; h = ((h & 0xFFFFFF) * 0xEBCA6B) & M
+        h ^= h >> 13; h = ((h & 0xFFFFFF) * 0xB2AE35) & M
+    else:
+        h ^= h >> 16; h = (h * 0x85EBCA6B) & M
+        h ^= h >> 13; h = (h * 0xC2B2AE35) & M
     h ^= h >> 16
     byte = (h >> ((c & 3) * 8)) & 0xFF
+    if attn:
+        return (byte & 0x7F) >= int(p * 128 + 0.5)
     return byte >= int(p * 256 + 0.5)
 
 
@@ -172,7 +180,7 @@ def test_attention_dropout_exact_mask(dtype, D, L):
     q, k, v = [t.detach().clone().requires_grad_(True)
                for t in qkv.float().reshape(N, L, 3, H, D).permute(2, 0, 3, 1, 4)]
     rows = np.arange(N * H * L)
-    keep = torch.from_numpy(_np_keep(rows, np.arange(L), p, seed)).reshape(N, H, L, L)
+    keep = torch.from_numpy(_np_keep(rows, np.arange(L), p, seed, attn=True)).reshape(N, H, L, L)
     P = torch.softmax((q @ k.transpose(-1, -2)) / math.sqrt(D), -1)
     o_ref = (P * keep / (1 - p)) @ v
     o_ref_flat = o_ref.transpose(1, 2).reshape(N * L, H * D)
