@@ -44,6 +44,9 @@ def parse():
     ap.add_argument("--size", type=int, default=224)
     ap.add_argument("--mask-ratio", type=float, default=0.75)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--resident", default="",
+                    help="encoder stages kept resident in HBM (no checkpoint recompute): "
+                         "comma list, or 'none'; default: the model's auto policy")
     ap.add_argument("--probe", default="dec_attn_fwd",
                     help="kernel group timed with events for the roofline line")
     return ap.parse_args()
@@ -126,6 +129,12 @@ class Probe:
         return sum(s.elapsed_time(e) for s, e in self.pairs) / len(self.pairs)
 
 
+def resident_used(model, frames, S):
+    from ssl_mae_amd.tiny_vit import auto_resident_stages
+    r = model.encoder.resident_stages
+    return auto_resident_stages(frames, S, True, torch.device("cuda")) if r == "auto" else r
+
+
 def main():
     args = parse()
     from ssl_mae_amd import dist as smdist
@@ -153,6 +162,9 @@ def main():
            "training": {"batch_size": B, "lr": 5e-4, "log_interval": 20}}
     torch.manual_seed(1234)                      # identical initial weights on every replica
     model = build_model(cfg, dev).train()
+    if args.resident:
+        model.encoder.resident_stages = () if args.resident == "none" else \
+            tuple(int(v) for v in args.resident.split(","))
     torch.manual_seed(4321 + rank)               # per-rank mask stream
     opt = FusedAdamW(model.parameters(), lr=5e-4, weight_decay=0.05)
     scaler = GradScaler()
@@ -237,7 +249,8 @@ def main():
                                    "T=8, 224x224, mask 0.75, bf16 autocast",
                        "model": "tiny_vit_21m_variant + TinyVideoMAE", "global_batch": B * world,
                        "per_gpu_batch": B, "frames": T, "image_size": S, "mask_ratio": r,
-                       "parallelism": f"dp{world}"},
+                       "parallelism": f"dp{world}",
+                       "resident_stages": list(resident_used(model, B * T, S))},
             "roofline": roof,
             "model_tflops_per_gpu": round(step_tflops, 1),
             "model_mfu": round(step_tflops / MFMA_BF16_PEAK_TFLOPS, 4),

@@ -131,7 +131,11 @@ class StemFn(torch.autograd.Function):
 # ============================================================================ MBConv
 class MBConvFn(torch.autograd.Function):
     """MBConv + SELayer (tiny_vit.py:36-56, 20-34): 1x1 expand, BN, GELU, dw3x3
-    (stride s), BN, GELU, SE, 1x1 project, BN (+ residual when s == 1, Cin == Cout)."""
+    (stride s), BN, GELU, SE, 1x1 project, BN (+ residual when s == 1, Cin == Cout).
+    st.bn_updates: how many times the BatchNorm running statistics take this batch
+    (2 reproduces a checkpointed stage's forward + recompute, TinyViT._run_stages);
+    st.recompute_a1: drop the expand output a1 (the block's largest tensor) and
+    recompute its GEMM in the backward (bit-identical: same kernel, same inputs)."""
 
     @staticmethod
     def forward(ctx, x, st, w_exp, g0, b0, w_dw, g2, b2, w_fc0, w_fc2, w_proj, g5, b5):
@@ -145,23 +149,24 @@ class MBConvFn(torch.autograd.Function):
         if fused:
             # BN0 + GELU folded into the depthwise conv's loads, BN2 statistics produced
             # by it, BN2 + GELU folded into the SE reads: no act(a1) / act(a2) in HBM
-            m0, r0 = K.bn_stats(a1, st.bn0.running_mean, st.bn0.running_var, st.bn0.momentum, st.bn0.eps, 1,
-                                st.bn0.num_batches_tracked)
+            m0, r0 = K.bn_stats(a1, st.bn0.running_mean, st.bn0.running_var, st.bn0.momentum, st.bn0.eps,
+                                st.bn_updates, st.bn0.num_batches_tracked)
             act0 = (m0, r0, g0.detach(), b0.detach(), True)
-            a2, m2, r2 = K.dwconv_fused(a1, act0, w_dw.detach().view(mid, 9), Fr, H, Wd, mid, s, bn_out=st.bn2)
+            a2, m2, r2 = K.dwconv_fused(a1, act0, w_dw.detach().view(mid, 9), Fr, H, Wd, mid, s, bn_out=st.bn2,
+                                        bn_updates=st.bn_updates)
             act2 = (m2, r2, g2.detach(), b2.detach(), True)
             h3, pooled, h1se, gate = K.se_fwd(a2, Fr, Ho * Wo, mid, w_fc0.detach(), w_fc2.detach(), act=act2)
         else:
-            h1, m0, r0 = _bn_forward(a1, st.bn0, gelu=True)
+            h1, m0, r0 = _bn_forward(a1, st.bn0, gelu=True, updates=st.bn_updates)
             a2 = K.dwconv(h1, w_dw.detach().view(mid, 9), Fr, H, Wd, mid, s)
             del h1
-            h2, m2, r2 = _bn_forward(a2, st.bn2, gelu=True)
+            h2, m2, r2 = _bn_forward(a2, st.bn2, gelu=True, updates=st.bn_updates)
             h3, pooled, h1se, gate = K.se_fwd(h2, Fr, Ho * Wo, mid, w_fc0.detach(), w_fc2.detach())
             del h2
         a3 = K.linear(h3, W(w_proj, mode).view(Cout, mid))
         del h3
-        mean5, rstd5 = K.bn_stats(a3, st.bn5.running_mean, st.bn5.running_var, st.bn5.momentum, st.bn5.eps, 1,
-                                  st.bn5.num_batches_tracked)
+        mean5, rstd5 = K.bn_stats(a3, st.bn5.running_mean, st.bn5.running_var, st.bn5.momentum, st.bn5.eps,
+                                  st.bn_updates, st.bn5.num_batches_tracked)
         out = K.bn_apply(a3, mean5, rstd5, g5.detach(), b5.detach(), residual=x2d if st.res else None,
                          row_scale=st.dp_scale, rows_per_group=Ho * Wo)
         m5, r5 = mean5, rstd5
@@ -169,7 +174,8 @@ class MBConvFn(torch.autograd.Function):
         ctx.st = st
         ctx.geom = (Fr, H, Wd, Cin, Ho, Wo)
         ctx.params = (w_exp, g0, b0, w_dw, g2, b2, w_fc0, w_fc2, w_proj, g5, b5)
-        ctx.save_for_backward(x, a1, a2, a3, m0, r0, m2, r2, m5, r5, pooled, h1se, gate)
+        ctx.save_for_backward(x, None if st.recompute_a1 else a1, a2, a3, m0, r0, m2, r2, m5, r5, pooled, h1se,
+                              gate)
         return out.view(Fr, Ho, Wo, Cout)
 
     @staticmethod
@@ -205,6 +211,8 @@ class MBConvFn(torch.autograd.Function):
         K.gemm(dz1, pooled, G(w_fc0), R, mid, Fr, 1, 1, R, mid, mid, beta=1.0)
         da2 = K.bn_bwd(dh2, a2, m2, r2, g2.detach(), b2.detach(), True, G(g2), G(b2))
         del dh2
+        if a1 is None:
+            a1 = K.linear(x.reshape(-1, Cin), W(w_exp, mode).view(mid, Cin))
         if ctx.fused:
             act0 = (m0, r0, g0.detach(), b0.detach(), True)
             dh1 = K.dwconv_fused_bwd(da2, a1, act0, w_dw.detach().view(mid, 9), G(w_dw).view(mid, 9), Fr, H, Wd,

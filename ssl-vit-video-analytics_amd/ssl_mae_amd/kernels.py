@@ -268,9 +268,10 @@ def _act_args(act):
     return [ptr(mean), ptr(rstd), ptr(w), ptr(b), 1 if gelu else 0]
 
 
-def dwconv_fused(x, act, w, F, H, W, C, stride, bn_out=None):
+def dwconv_fused(x, act, w, F, H, W, C, stride, bn_out=None, bn_updates=1):
     """y = dwconv3x3(act(x)) (bf16); with bn_out (a BatchNorm2d module) also its
-    train-mode statistics of y: returns (y, mean, rstd) (or y)."""
+    train-mode statistics of y (running stats updated bn_updates times): returns
+    (y, mean, rstd) (or y)."""
     _chk(x)
     Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
     dev = x.device
@@ -290,7 +291,7 @@ def dwconv_fused(x, act, w, F, H, W, C, stride, bn_out=None):
     ws = _ws(nbytes, dev)
     call("sm_bn_stats_from_partials", ptr(part), part.shape[0], C, F * Ho * Wo, ptr(mean), ptr(rstd),
          ptr(bn_out.running_mean), ptr(bn_out.running_var), ptr(bn_out.num_batches_tracked),
-         float(bn_out.momentum), float(bn_out.eps), 1, ptr(ws), nbytes, stream())
+         float(bn_out.momentum), float(bn_out.eps), int(bn_updates), ptr(ws), nbytes, stream())
     return y, mean, rstd
 
 

@@ -81,11 +81,12 @@ class MBConv(nn.Module):
             Conv2d_BN(mid, out_chans, ks=1, bn_weight_init=0))
         self.drop_path = DropPath(drop_path) if drop_path > 0.0 else nn.Identity()
 
-    def run(self, x, mode):
+    def run(self, x, mode, resident=False):
         c = self.conv
         dps = droppath_scale(self, x.shape[0], mode, 0, x.device) if self.use_res_connect else None
         st = _St(mode=mode, mid=self.mid, cout=self.out_chans, stride=self.stride, res=self.use_res_connect,
-                 bn0=c[0].bn, bn2=c[2].bn, bn5=c[5].bn, dp_scale=dps)
+                 bn0=c[0].bn, bn2=c[2].bn, bn5=c[5].bn, dp_scale=dps, bn_updates=2 if resident else 1,
+                 recompute_a1=resident)
         return MBConvFn.apply(x, st, c[0].c.weight, c[0].bn.weight, c[0].bn.bias, c[2].c.weight, c[2].bn.weight,
                               c[2].bn.bias, c[4].fc[0].weight, c[4].fc[2].weight, c[5].c.weight, c[5].bn.weight,
                               c[5].bn.bias)
@@ -146,7 +147,7 @@ class TinyViTBlock(nn.Module):
         self.norm2 = nn.LayerNorm(dim)
         self.mlp = Mlp(in_features=dim, hidden_features=int(dim * mlp_ratio))
 
-    def run(self, x, mode):
+    def run(self, x, mode, resident=False):   # no BatchNorm, nothing to trade: resident unused
         Fr, H, Wd, C = x.shape
         st = _St(mode=mode, N=Fr, L=H * Wd, heads=self.num_heads, head_dim=C // self.num_heads,
                  eps=self.norm1.eps, attn_drop=0.0, seed_attn=0, drop1=0.0, seed1=0, drop_ff=0.0, seed_ff=0,
@@ -160,9 +161,9 @@ class TinyViTBlock(nn.Module):
 
 
 class _Stage(nn.Sequential):
-    def run(self, x, mode):
+    def run(self, x, mode, resident=False):
         for blk in self:
-            x = blk.run(x, mode)
+            x = blk.run(x, mode, resident)
         return x
 
 
@@ -173,6 +174,10 @@ class TinyViT(nn.Module):
                  num_heads=[3, 6, 12, 24], window_sizes=[7, 7, 14, 7], drop_path_rate=0.1, use_checkpoint=True):
         super().__init__()
         self.use_checkpoint = use_checkpoint
+        # Stages whose activations stay resident in HBM instead of being dropped and
+        # recomputed under use_checkpoint (see _run_stages): a tuple, or "auto"
+        # (auto_resident_stages: as many as the device memory holds).
+        self.resident_stages = "auto"
         self.embed_dims = list(embed_dims)
         self.patch_embed = PatchEmbed(in_chans, embed_dims[0])
         self.stages = nn.ModuleList()
@@ -198,10 +203,25 @@ class TinyViT(nn.Module):
         return Mode(torch.is_autocast_enabled("cuda"), next_seed_base(self))
 
     def _run_stages(self, x, n_stages, mode):
+        """tiny_vit.py:170-175: each stage under checkpoint(use_reentrant=False) when
+        training with use_checkpoint.  A stage listed in resident_stages keeps its
+        activations in HBM instead (288 GB holds them at the bench batch): no
+        recompute, and its BatchNorms take the batch statistics twice, which is what
+        the reference's checkpoint forward + recompute does to the running stats
+        (num_batches_tracked += 2).  Every output, gradient and buffer is identical;
+        only the memory/time trade changes.  (An MBConv in a resident stage still
+        drops its 4x-wide expand output and recomputes that one GEMM.)"""
+        resident = self.resident_stages
+        if resident == "auto":
+            resident = auto_resident_stages(x.shape[0], x.shape[1] * 2, mode.bf16, x.device) \
+                if self.use_checkpoint and self.training else ()
         for i in range(n_stages):
             stage = self.stages[i]
             if self.use_checkpoint and self.training:
-                x = checkpoint.checkpoint(stage.run, x, mode, use_reentrant=False)
+                if i in resident:
+                    x = stage.run(x, mode, resident=True)
+                else:
+                    x = checkpoint.checkpoint(stage.run, x, mode, use_reentrant=False)
             else:
                 x = stage.run(x, mode)
         return x
@@ -230,6 +250,23 @@ class TinyViT(nn.Module):
         t = self.patch_embed.run(x, mode)
         t = self._run_stages(t, 4, mode)
         return t.permute(0, 3, 1, 2)
+
+
+# Peak HBM of one MAE training step per frame (GiB, bf16, 224x224 frames, measured
+# with bench.py at B=256 clips x T=8 on MI355X) for each resident-stage policy;
+# activations scale with the pixel count, fp32 doubles them.
+_PEAK_GIB_PER_FRAME = {(1, 2): 216.0 / 2048, (2,): 171.9 / 2048, (): 143.6 / 2048}
+
+
+def auto_resident_stages(frames, image_size, bf16, device, budget=0.85):
+    """The largest resident set whose predicted step peak fits `budget` of the
+    device memory (stage 0, the 112x112 MBConvs, is always recomputed)."""
+    total = torch.cuda.get_device_properties(device).total_memory / 2 ** 30
+    scale = frames * (image_size / 224.0) ** 2 * (1 if bf16 else 2)
+    for policy in ((1, 2), (2,)):
+        if _PEAK_GIB_PER_FRAME[policy] * scale <= budget * total:
+            return policy
+    return ()
 
 
 def index_modules(root):

@@ -71,12 +71,16 @@ def _run_steps(model, d, steps, bf16=False):
 GOLD = ["step_b2_t2_s32", "step_b2_t4_s64", "step_b1_t8_s224"]
 
 
+@pytest.mark.parametrize("resident", [(), (0, 1, 2)])
 @pytest.mark.parametrize("case", GOLD)
-def test_fp32_step_matches_reference_golden(golden_dir, case):
+def test_fp32_step_matches_reference_golden(golden_dir, case, resident):
+    """resident=(0, 1, 2): every stage kept in HBM (no checkpoint recompute) must give
+    the same loss, gradients, parameters and BN running stats (updated twice)."""
     d = np.load(os.path.join(golden_dir, case + ".npz"))
     B, T, S = int(d["B"]), int(d["T"]), int(d["S"])
     cfg = _cfg(B, T, S, float(d["ratio"]))
     model = _build(cfg)
+    model.encoder.resident_stages = resident
     # mask parity first (bit-exact): same seed, same RNG stream as the reference's step
     from ssl_mae_amd.mae_loader import get_tube_mask
     torch.manual_seed(42)
