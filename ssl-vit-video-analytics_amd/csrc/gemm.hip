@@ -10,7 +10,8 @@
 // Linear dX   dX = dY W      : (a 0, b 1)
 // Linear dW   dW = dY^T X    : (a 1, b 1)   -> split-K over the token axis
 //
-// bf16 path: 128x128x64 block tile, 4 waves (2x2), each wave 64x64 = 2x2
+// bf16 path (gemm_bf16_kernel; gemm_bf16_v2 below is the default, see there):
+// 128x128x64 block tile, 4 waves (2x2), each wave 64x64 = 2x2
 // v_mfma_f32_32x32x16_bf16 tiles.  K-contiguous operands are staged to an
 // XOR-swizzled [row][64] LDS image read with ds_read_b128; M/N-contiguous operands
 // are staged as a [k][128] image and read with ds_read_b64_tr_b16 (hardware
@@ -19,6 +20,7 @@
 // f32 path (parity mode): 64x64x16 tile on v_mfma_f32_32x32x2_f32 (exact fp32).
 #include "common.h"
 #include "sm_api.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -330,6 +332,155 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
   gemm_epilogue<TC, VEC>(g, acc, m0, n0, wm, wn, l);
 }
 
+// ============================================================ bf16 MFMA kernel, v2
+// BM x 128 block tile, BK = 64, each wave 64 x 64 (2 x 2 v_mfma_f32_32x32x16_bf16):
+// BM = 256 -> 8 waves (4 along M x 2 along N, 512 threads), BM = 128 -> 4 waves.
+// Operands are staged with raw buffer loads: each thread's chunk offsets are 32-bit
+// voffsets computed once, the K advance moves the wave-uniform base of the buffer
+// descriptor, and rows / columns past the matrix or the K tail read as zero through
+// an out-of-range voffset.  The main loop therefore carries no per-step address
+// arithmetic in VGPRs (the first kernel spent ~10 VALU instructions per MFMA on 64-bit
+// pointer updates and zero-fill moves), which frees the registers for 4 waves per
+// SIMD at BM = 256.
+constexpr uint32_t BUF_OOB = 0x40000000u;   // >= num_records: the load returns 0
+
+template <int ROWS>
+SM_DEV int mnmaj_off_r(int krow, int col) {   // [64][ROWS] MN-major tile (ROWS*2-B rows)
+  return krow * (ROWS * 2) + ((((col >> 3) ^ ((krow & 3) << 2))) << 4) + ((col & 7) << 1);
+}
+
+template <int ROWS, int NT, bool KMAJ>
+struct TileLoader {
+  static constexpr int CH = ROWS * 64 * 2 / 16 / NT;   // 16-B chunks per thread per tile
+  static constexpr int KSTEP = NT / (ROWS / 8);        // MN-major: k rows between chunks
+  static constexpr int LSTEP = KMAJ ? (NT / 8) * 128 : KSTEP * ROWS * 2;
+  uint32_t voff[CH];
+  int loff0, kk0;
+  // lines: rows (K-major) or columns (MN-major) of this panel that exist
+  SM_DEV void init(int64_t ld, int lines) {
+    const int t = threadIdx.x;
+    if (KMAJ) {
+      const int row = t >> 3, ch = t & 7;
+      kk0 = ch * 8;
+      loff0 = kmaj_off(row, ch);   // rows row + (NT/8) i keep the swizzle: + i * LSTEP
+#pragma unroll
+      for (int i = 0; i < CH; ++i) {
+        const int r = row + (NT / 8) * i;
+        voff[i] = r < lines ? (uint32_t)(((int64_t)r * ld + kk0) * 2) : BUF_OOB;
+      }
+    } else {
+      const int kk = t / (ROWS / 8), col = (t % (ROWS / 8)) * 8;
+      kk0 = kk;
+      loff0 = mnmaj_off_r<ROWS>(kk, col);
+#pragma unroll
+      for (int i = 0; i < CH; ++i)
+        voff[i] = col < lines ? (uint32_t)(((int64_t)(kk + KSTEP * i) * ld + col) * 2) : BUF_OOB;
+    }
+  }
+  SM_DEV void load(__amdgpu_buffer_rsrc_t rs, int kvalid, uint4 (&r)[CH]) const {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int k = KMAJ ? kk0 : kk0 + KSTEP * i;
+      const uint32_t o = k < kvalid ? voff[i] : BUF_OOB;
+      r[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0));
+    }
+  }
+  SM_DEV void store(char* lds, const uint4 (&r)[CH]) const {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) *(uint4*)(lds + loff0 + i * LSTEP) = r[i];
+  }
+};
+
+// descriptor over a panel whose K-step k0 starts at element `off` of P
+SM_DEV __amdgpu_buffer_rsrc_t panel_rsrc(const __bf16* P, int64_t off) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(P + off), (short)0, (int)BUF_OOB, 0x00020000);
+}
+
+template <bool KMAJ, int ROWS>
+SM_DEV bf16x8 lread_frag_r(const char* lds, int rb, int s) {
+  const int l = threadIdx.x & 63;
+  if (KMAJ) {
+    return *(const bf16x8*)(lds + kmaj_off(rb + (l & 31), 2 * s + (l >> 5)));
+  } else {
+    const int h = l >> 5, g1 = (l >> 4) & 1, i = l & 15, q = i >> 2, p = i & 3;
+    const int col = rb + 16 * g1 + 4 * p;
+    const int k0 = 16 * s + 8 * h + q;
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + mnmaj_off_r<ROWS>(k0, col)));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + mnmaj_off_r<ROWS>(k0 + 4, col)));
+    typedef __attribute__((ext_vector_type(8))) short s16x8;
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+template <bool AK, bool BK, typename TC, bool VEC, int BMV>
+__global__ __launch_bounds__(BMV * 2, BMV == 256 ? 4 : 2) void gemm_bf16_v2(GemmArgs g) {
+  constexpr int NT = BMV * 2, BNV = 128;
+  __shared__ __attribute__((aligned(16))) char lds[(BMV + BNV) * BKT * 2];
+  char* la = lds;
+  char* lb = lds + BMV * BKT * 2;
+  const int ntn = (g.N + BNV - 1) / BNV;
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int m0 = (tile / ntn) * BMV, n0 = (tile % ntn) * BNV;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
+  const __bf16* A = (const __bf16*)g.A;
+  const __bf16* B = (const __bf16*)g.B;
+  const int kb = g.k_begin + blockIdx.z * g.k_chunk;
+  const int ke = min(g.K, kb + g.k_chunk);
+
+  TileLoader<BMV, NT, AK> tla;
+  TileLoader<BNV, NT, BK> tlb;
+  tla.init(g.lda, g.M - m0);
+  tlb.init(g.ldb, g.N - n0);
+  // element offset of K-step k0 of each panel
+  const int64_t abase = AK ? (int64_t)m0 * g.lda : (int64_t)m0;
+  const int64_t bbase = BK ? (int64_t)n0 * g.ldb : (int64_t)n0;
+  const int64_t astep = AK ? 1 : g.lda, bstep = BK ? 1 : g.ldb;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  uint4 ra[TileLoader<BMV, NT, AK>::CH], rb[TileLoader<BNV, NT, BK>::CH];
+  if (kb < ke) {
+    tla.load(panel_rsrc(A, abase + kb * astep), ke - kb, ra);
+    tlb.load(panel_rsrc(B, bbase + kb * bstep), ke - kb, rb);
+  }
+  for (int k0 = kb; k0 < ke; k0 += BKT) {
+    tla.store(la, ra);
+    tlb.store(lb, rb);
+    __syncthreads();
+    if (k0 + BKT < ke) {
+      tla.load(panel_rsrc(A, abase + (k0 + BKT) * astep), ke - k0 - BKT, ra);
+      tlb.load(panel_rsrc(B, bbase + (k0 + BKT) * bstep), ke - k0 - BKT, rb);
+    }
+#pragma unroll
+    for (int s = 0; s < BKT / 16; ++s) {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = lread_frag_r<AK, BMV>(la, wm + 32 * i, s);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfr[j] = lread_frag_r<BK, BNV>(lb, wn + 32 * j, s);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  gemm_epilogue<TC, VEC>(g, acc, m0, n0, wm, wn, l);
+}
+
 // ============================================================ f32 MFMA kernel
 constexpr int FBM = 64, FBN = 64, FBK = 16, FLD = 64 + 4;
 
@@ -409,8 +560,10 @@ __global__ void splitk_reduce_kernel(GemmArgs g, int splits) {
   }
 }
 
+int variant_bm(int v);
+int gemm_variant(int M);
 int choose_splits(int M, int N, int K, bool bf16) {
-  const int bm = bf16 ? BM : FBM, bn = bf16 ? BN : FBN, bk = bf16 ? BKT : FBK;
+  const int bm = bf16 ? variant_bm(gemm_variant(M)) : FBM, bn = bf16 ? BN : FBN, bk = bf16 ? BKT : FBK;
   const int64_t tiles = (int64_t)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   if (tiles >= 512 || K < 4096) return 1;
   int64_t want = (1024 + tiles - 1) / tiles;
@@ -420,17 +573,41 @@ int choose_splits(int M, int N, int K, bool bf16) {
   return s < 1 ? 1 : (int)s;
 }
 
+// bf16 kernel variant: 1 = gemm_bf16_kernel (128 x 128, 4 waves), 2 = gemm_bf16_v2 at
+// BM = 256 (8 waves), 3 = gemm_bf16_v2 at BM = 128.  Default (0): v2, BM = 256 when
+// M >= 192 (a 256-row tile half empty loses to BM = 128 there: dW of the 96-channel
+// MBConv projection).  SM_GEMM_VARIANT pins one (A/B measurement runs).
+int gemm_variant(int M) {
+  static const int forced = [] {
+    const char* e = getenv("SM_GEMM_VARIANT");
+    const int x = e ? atoi(e) : 0;
+    return (x >= 1 && x <= 3) ? x : 0;
+  }();
+  if (forced) return forced;
+  return M >= 192 ? 2 : 3;
+}
+int variant_bm(int v) { return v == 2 ? 256 : 128; }
+
+template <bool AK, bool BK, typename TC, bool VEC>
+void launch_bf16(const GemmArgs& g, int splits, hipStream_t st) {
+  const int v = gemm_variant(g.M);
+  const int bm = variant_bm(v);
+  dim3 grid(((g.N + BN - 1) / BN) * ((g.M + bm - 1) / bm), 1, splits);
+  if (v == 1) hipLaunchKernelGGL((gemm_bf16_kernel<AK, BK, TC, VEC>), grid, dim3(256), 0, st, g);
+  else if (v == 2) hipLaunchKernelGGL((gemm_bf16_v2<AK, BK, TC, VEC, 256>), grid, dim3(512), 0, st, g);
+  else hipLaunchKernelGGL((gemm_bf16_v2<AK, BK, TC, VEC, 128>), grid, dim3(256), 0, st, g);
+}
+
 template <bool AK, bool BK>
 int launch_layout(int abt, int ct, GemmArgs g, int splits, hipStream_t st) {
   if (abt == SM_BF16) {
-    dim3 grid(((g.N + BN - 1) / BN) * ((g.M + BM - 1) / BM), 1, splits);
     const bool vec = !((g.N & 7) || (!g.partial && (g.ldc & 7)));
     if (ct == SM_BF16) {
-      if (vec) hipLaunchKernelGGL((gemm_bf16_kernel<AK, BK, __bf16, true>), grid, dim3(256), 0, st, g);
-      else hipLaunchKernelGGL((gemm_bf16_kernel<AK, BK, __bf16, false>), grid, dim3(256), 0, st, g);
+      if (vec) launch_bf16<AK, BK, __bf16, true>(g, splits, st);
+      else launch_bf16<AK, BK, __bf16, false>(g, splits, st);
     } else {
-      if (vec) hipLaunchKernelGGL((gemm_bf16_kernel<AK, BK, float, true>), grid, dim3(256), 0, st, g);
-      else hipLaunchKernelGGL((gemm_bf16_kernel<AK, BK, float, false>), grid, dim3(256), 0, st, g);
+      if (vec) launch_bf16<AK, BK, float, true>(g, splits, st);
+      else launch_bf16<AK, BK, float, false>(g, splits, st);
     }
   } else {
     if (ct != SM_F32) return -3;
