@@ -129,10 +129,62 @@ SM_DEV bf16x8 lread_frag(const char* lds, int rb, int s) {
   }
 }
 
-// Epilogue of one 128x128 tile from the (swapped-operand) accumulators.
-template <typename TC, bool VEC>
-SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[2][2], int m0, int n0,
-                                                         int wm, int wn, int l) {
+// Row-staged stores (gemm_bf16_v2).  A row run is 8 consecutive columns of one output
+// row held by one lane; stored straight from the lanes, a store instruction covers 32
+// rows x 32 B (32 partial cache lines).  Staged, each wave writes its runs into a
+// 32-row x 128-B LDS image (chunk index XOR-swizzled with (row >> 1) & 7: conflict-free
+// both ways) and stores it back as 8 rows x 128 B per instruction (whole lines).
+struct RowStage {
+  char* base;   // this wave's 2 x 4 KB: [0] C, [1] aux
+  SM_DEV void put(int region, int row, int chunk, uint4 v) const {
+    *(uint4*)(base + region * 4096 + row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4)) = v;
+  }
+  // rows: tile rows [row0, row0 + 32) of out (ld elements) at column col0; 16-B chunk
+  // c holds `cpc` columns; rows >= M or chunk columns >= N are not stored
+  template <typename TC>
+  SM_DEV void flush(int region, TC* out, int64_t ld, int64_t row0, int col0, int M, int N, int l) const {
+    constexpr int cpc = 16 / sizeof(TC);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int c = l & 7;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = (l >> 3) + 8 * q;
+      const uint4 v = *(const uint4*)(base + region * 4096 + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+      const int64_t row = row0 + r;
+      const int col = col0 + c * cpc;
+      if (row < M && col < N) *(uint4*)(out + row * ld + col) = v;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+};
+SM_DEV uint4 pack8(const float* v, __bf16*) {
+  bf16x8 a;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = (__bf16)v[i];
+  return __builtin_bit_cast(uint4, a);
+}
+
+// one 8-column run (row l & 31 of the wave's 32-row slice) into the stage image:
+// bf16 -> chunk 4j + 2p + h of a 64-column image; fp32 -> chunks 4p + 2h, +1 of a
+// 32-column image (one per j)
+template <typename TC>
+SM_DEV void stage_put(const RowStage& rs, int region, int j, int p, int h, int l, const float* v) {
+  const int row = l & 31;
+  if (sizeof(TC) == 2) {
+    rs.put(region, row, 4 * j + 2 * p + h, pack8(v, (__bf16*)nullptr));
+  } else {
+    rs.put(region, row, 4 * p + 2 * h, make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]),
+                                                  __float_as_uint(v[2]), __float_as_uint(v[3])));
+    rs.put(region, row, 4 * p + 2 * h + 1, make_uint4(__float_as_uint(v[4]), __float_as_uint(v[5]),
+                                                      __float_as_uint(v[6]), __float_as_uint(v[7])));
+  }
+}
+
+// Epilogue of one wave's (32 MI) x (32 NJ) tile from the (swapped-operand) accumulators.  stage:
+// non-null -> RowStage stores (VEC, non-split-K path).
+template <typename TC, bool VEC, int MI = 2, int NJ = 2>
+SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[MI][NJ], int m0, int n0,
+                                                         int wm, int wn, int l, char* stage = nullptr) {
   // The MFMAs run with swapped operands (D = B_frag x A_frag), so each lane owns
   // one output ROW (token) and registers r hold its columns
   // wn + 32j + (r&3) + 8(r>>2) + 4h: row-per-lane, no LDS round trip.
@@ -140,11 +192,11 @@ SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x
   const int64_t rbase = m0 + wm + (l & 31);
   if (!VEC) {   // N % 8 or ldc % 8 != 0 (launch-uniform; chosen at launch)
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < MI; ++i) {
       const int64_t row = rbase + 32 * i;
       if (row >= g.M) continue;
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int col = n0 + wn + 32 * j + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -158,9 +210,9 @@ SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x
   // values acc[i][j][8p + 0..3] and acc[i][j][8p + 4..7].  All epilogue math is
   // per element on those runs; each run is one 16-B (bf16) / 32-B (fp32) store.
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int p = 0; p < 2; ++p)
 #pragma unroll
@@ -173,11 +225,11 @@ SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x
   if (g.partial) {   // split-K: raw fp32 runs into this z's slab
     float* slab = g.partial + (int64_t)blockIdx.z * g.M * g.N;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < MI; ++i) {
       const int64_t row = rbase + 32 * i;
       if (row >= g.M) continue;
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
           const int col = n0 + wn + 32 * j + 16 * p + 8 * h;
@@ -191,6 +243,7 @@ SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x
     }
     return;
   }
+  const RowStage rs_{stage};
   const bool bias_vec = g.bias && ((uintptr_t)g.bias & 15) == 0;
   const bool has_r = g.beta != 0.f;
   const TC* Rsrc = g.R ? (const TC*)g.R : (const TC*)g.C;
@@ -198,19 +251,20 @@ SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x
   const float ks = g.drop_p > 0.f ? 1.f / (1.f - g.drop_p) : 1.f;
   constexpr int RW = sizeof(TC) * 8 / 16;   // 16-B words per 8-column run
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < MI; ++i) {
     const int64_t row = rbase + 32 * i;
-    if (row >= g.M) continue;
-    const float rs = g.row_scale ? g.row_scale[row / g.rows_per_group] : 1.f;
+    const bool rok = row < g.M;   // (staged: out-of-range lanes still take part in the flushes)
+    if (!rok && !stage) continue;
+    const float rs = (g.row_scale && rok) ? g.row_scale[row / g.rows_per_group] : 1.f;
     const uint32_t rb = drop_rowbase(s32, (uint64_t)row);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       uint4 rr[2][RW];   // the residual runs of this (row, j), in flight before the stores (R may alias C)
       if (has_r) {
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
           const int col = n0 + wn + 32 * j + 16 * p + 8 * h;
-          if (col < g.N) {
+          if (col < g.N && rok) {
             const uint4* src = (const uint4*)(Rsrc + row * g.ldc + col);
 #pragma unroll
             for (int q = 0; q < RW; ++q) rr[p][q] = src[q];
@@ -220,7 +274,7 @@ SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
         const int col = n0 + wn + 32 * j + 16 * p + 8 * h;
-        if (col >= g.N) continue;
+        if (col >= g.N || !rok) continue;
         float b8[8];
         if (bias_vec) {
           const float4 b0 = *(const float4*)(g.bias + col);
@@ -241,7 +295,10 @@ SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x
         }
         const int64_t idx = row * g.ldc + col;
         if (g.epi & 1) {
-          if (g.aux) store8((TC*)g.aux + idx, v);
+          if (g.aux) {
+            if (stage) stage_put<TC>(rs_, 1, j, p, h, l, v);
+            else store8((TC*)g.aux + idx, v);
+          }
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = gelu_f(v[e]);
         }
@@ -263,8 +320,21 @@ SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = fmaf(g.beta, r8[e], v[e]);
         }
-        store8((TC*)g.C + idx, v);
+        if (stage) stage_put<TC>(rs_, 0, j, p, h, l, v);
+        else store8((TC*)g.C + idx, v);
       }
+      if (stage && sizeof(TC) == 4) {   // fp32: one 32-column (128-B) image per (i, j)
+        const int64_t r0 = m0 + wm + 32 * i;
+        const int c0 = n0 + wn + 32 * j;
+        if (g.aux && (g.epi & 1)) rs_.flush<TC>(1, (TC*)g.aux, g.ldc, r0, c0, g.M, g.N, l);
+        rs_.flush<TC>(0, (TC*)g.C, g.ldc, r0, c0, g.M, g.N, l);
+      }
+    }
+    if (stage && sizeof(TC) == 2) {     // bf16: one 64-column (128-B) image per i
+      const int64_t r0 = m0 + wm + 32 * i;
+      const int c0 = n0 + wn;
+      if (g.aux && (g.epi & 1)) rs_.flush<TC>(1, (TC*)g.aux, g.ldc, r0, c0, g.M, g.N, l);
+      rs_.flush<TC>(0, (TC*)g.C, g.ldc, r0, c0, g.M, g.N, l);
     }
   }
 }
@@ -417,7 +487,8 @@ SM_DEV bf16x8 lread_frag_r(const char* lds, int rb, int s) {
 template <bool AK, bool BK, typename TC, bool VEC, int BMV>
 __global__ __launch_bounds__(BMV * 2, BMV == 256 ? 4 : 2) void gemm_bf16_v2(GemmArgs g) {
   constexpr int NT = BMV * 2, BNV = 128;
-  __shared__ __attribute__((aligned(16))) char lds[(BMV + BNV) * BKT * 2];
+  constexpr int LDS_MAIN = (BMV + BNV) * BKT * 2, LDS_EPI = (NT / 64) * 8192;   // operand tiles | row stage
+  __shared__ __attribute__((aligned(16))) char lds[LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI];
   char* la = lds;
   char* lb = lds + BMV * BKT * 2;
   const int ntn = (g.N + BNV - 1) / BNV;
@@ -478,7 +549,7 @@ __global__ __launch_bounds__(BMV * 2, BMV == 256 ? 4 : 2) void gemm_bf16_v2(Gemm
     }
     __syncthreads();
   }
-  gemm_epilogue<TC, VEC>(g, acc, m0, n0, wm, wn, l);
+  gemm_epilogue<TC, VEC>(g, acc, m0, n0, wm, wn, l, lds + w * 8192);
 }
 
 // ============================================================ f32 MFMA kernel
@@ -561,9 +632,11 @@ __global__ void splitk_reduce_kernel(GemmArgs g, int splits) {
 }
 
 int variant_bm(int v);
-int gemm_variant(int M);
+int variant_bn(int v);
+int gemm_variant(int M, int N);
 int choose_splits(int M, int N, int K, bool bf16) {
-  const int bm = bf16 ? variant_bm(gemm_variant(M)) : FBM, bn = bf16 ? BN : FBN, bk = bf16 ? BKT : FBK;
+  const int v = gemm_variant(M, N);
+  const int bm = bf16 ? variant_bm(v) : FBM, bn = bf16 ? variant_bn(v) : FBN, bk = bf16 ? BKT : FBK;
   const int64_t tiles = (int64_t)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   if (tiles >= 512 || K < 4096) return 1;
   int64_t want = (1024 + tiles - 1) / tiles;
@@ -574,10 +647,12 @@ int choose_splits(int M, int N, int K, bool bf16) {
 }
 
 // bf16 kernel variant: 1 = gemm_bf16_kernel (128 x 128, 4 waves), 2 = gemm_bf16_v2 at
-// BM = 256 (8 waves), 3 = gemm_bf16_v2 at BM = 128.  Default (0): v2, BM = 256 when
+// BM = 256 (8 waves), 3 = gemm_bf16_v2 at BM = 128.  (A 256 x 256 tile fed by LDS-DMA,
+// double-buffered, 1 block / CU, measured 5-45 % slower than variant 2 on every
+// shape of the step, so it was dropped.)  Default (0): v2, BM = 256 when
 // M >= 192 (a 256-row tile half empty loses to BM = 128 there: dW of the 96-channel
 // MBConv projection).  SM_GEMM_VARIANT pins one (A/B measurement runs).
-int gemm_variant(int M) {
+int gemm_variant(int M, int N) {
   static const int forced = [] {
     const char* e = getenv("SM_GEMM_VARIANT");
     const int x = e ? atoi(e) : 0;
@@ -585,14 +660,16 @@ int gemm_variant(int M) {
   }();
   if (forced) return forced;
   return M >= 192 ? 2 : 3;
+  (void)N;
 }
 int variant_bm(int v) { return v == 2 ? 256 : 128; }
+int variant_bn(int v) { return 128; (void)v; }
 
 template <bool AK, bool BK, typename TC, bool VEC>
 void launch_bf16(const GemmArgs& g, int splits, hipStream_t st) {
-  const int v = gemm_variant(g.M);
-  const int bm = variant_bm(v);
-  dim3 grid(((g.N + BN - 1) / BN) * ((g.M + bm - 1) / bm), 1, splits);
+  const int v = gemm_variant(g.M, g.N);
+  const int bm = variant_bm(v), bn = variant_bn(v);
+  dim3 grid(((g.N + bn - 1) / bn) * ((g.M + bm - 1) / bm), 1, splits);
   if (v == 1) hipLaunchKernelGGL((gemm_bf16_kernel<AK, BK, TC, VEC>), grid, dim3(256), 0, st, g);
   else if (v == 2) hipLaunchKernelGGL((gemm_bf16_v2<AK, BK, TC, VEC, 256>), grid, dim3(512), 0, st, g);
   else hipLaunchKernelGGL((gemm_bf16_v2<AK, BK, TC, VEC, 128>), grid, dim3(256), 0, st, g);
