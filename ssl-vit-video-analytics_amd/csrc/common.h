@@ -62,28 +62,26 @@ SM_DEV void store4(__bf16* p, const float* v) {
 
 // ---------------------------------------------------------------- math
 // Exact (erf) GELU, nn.GELU's default.  Phi(x) = 0.5 (1 + erf(x / sqrt 2)) is formed
-// from erfc(z), z = |x| / sqrt 2, with the Chebyshev-fitted erfc of Numerical Recipes
-// (fractional error < 1.2e-7 for all z >= 0): Phi = erfc / 2 for x < 0 (no
-// cancellation in the left tail) and 1 - erfc / 2 for x >= 0.  One rcp, one exp2 and
-// a 10-term Horner chain: about a third of the branch-free library erff.  Every kernel
-// (GEMM epilogue, BatchNorm apply / backward, fused depthwise / SE loads) uses these
-// two functions, so recomputed activations are bit-identical to stored ones.
+// from erfc(z), z = |x| / sqrt 2, as erfc(z) = t P5(t) exp(-z^2), t = 1 / (1 + 0.3275911 z)
+// (Abramowitz & Stegun 7.1.26, |error| < 1.5e-7): Phi = erfc / 2 for x < 0 (no
+// cancellation in the left tail) and 1 - erfc / 2 for x >= 0.  The exp(-z^2) =
+// exp(-x^2 / 2) factor is shared with the normal pdf of the derivative, so GELU is one
+// rcp, one exp2 and a 5-term Horner chain, and its derivative adds two ops.  (The
+// previous Numerical-Recipes erfc needed a 10-term chain and a second exp2; these
+// functions sit in the VALU-bound BatchNorm / depthwise / SE / GEMM-epilogue loops.)
+// Every kernel uses these two functions, so recomputed activations are bit-identical
+// to stored ones.
 SM_DEV float gelu_phi_pair(float x, float* pdf_out) {
   const float z = fabsf(x) * 0.70710678118654752f;
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, z, 1.0f));
-  float p = 0.17087277f;
-  p = fmaf(p, t, -0.82215223f);
-  p = fmaf(p, t, 1.48851587f);
-  p = fmaf(p, t, -1.13520398f);
-  p = fmaf(p, t, 0.27886807f);
-  p = fmaf(p, t, -0.18628806f);
-  p = fmaf(p, t, 0.09678418f);
-  p = fmaf(p, t, 0.37409196f);
-  p = fmaf(p, t, 1.00002368f);
-  p = fmaf(p, t, -1.26551223f);
-  const float e = __builtin_amdgcn_exp2f((p - z * z) * 1.44269504088896341f);
-  const float half_erfc = 0.5f * t * e;
-  if (pdf_out) *pdf_out = 0.39894228040143268f * __builtin_amdgcn_exp2f(-z * z * 1.44269504088896341f);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float p = 1.061405429f;
+  p = fmaf(p, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float e = __builtin_amdgcn_exp2f(z * z * -1.44269504088896341f);
+  const float half_erfc = 0.5f * (p * t) * e;
+  if (pdf_out) *pdf_out = 0.39894228040143268f * e;
   return x < 0.f ? half_erfc : 1.0f - half_erfc;
 }
 SM_DEV float gelu_f(float x) { return x * gelu_phi_pair(x, nullptr); }

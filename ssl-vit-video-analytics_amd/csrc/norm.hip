@@ -139,6 +139,149 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* dy, const TI* x, 
 
 
 
+// ---------------------------------------------- LayerNorm, 16 lanes per row (C = 192, 384)
+// Four rows per wave (one per 16-lane DPP row), 16 rows per block in flight, a block
+// walks a contiguous run of rows.  Lane gl of a row owns columns 64u + 4gl + j, so each
+// load / store instruction covers 4 rows x one contiguous 128-B (bf16) or 256-B (fp32)
+// run; gamma / beta live in registers for the whole run; row sums are 4 DPP adds
+// (row_mirror, row_half_mirror, quad swaps) instead of LDS shuffles.
+template <int CTRL>
+SM_DEV float dppf(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+SM_DEV float sum16(float v) {
+  v += dppf<0x140>(v);   // row_mirror
+  v += dppf<0x141>(v);   // row_half_mirror
+  v += dppf<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dppf<0xB1>(v);    // quad_perm [1,0,3,2]
+  return v;
+}
+
+template <typename TI, typename TO, int C>
+__global__ __launch_bounds__(256) void ln_fwd16_kernel(const TI* x, const float* g, const float* b, TO* y,
+                                                       float* mean, float* rstd, int64_t M, float eps,
+                                                       int64_t rows_per_block) {
+  constexpr int U = C / 64;
+  const int gl = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  float gg[U][4], bb[U][4];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    load4(g + 64 * u + 4 * gl, gg[u]);
+    load4(b + 64 * u + 4 * gl, bb[u]);
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
+  for (int64_t row = r0 + grp; row < r1; row += 16) {
+    const TI* xr = x + row * C + 4 * gl;
+    float v[U][4];
+    float s = 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      load4(xr + 64 * u, v[u]);
+      s += (v[u][0] + v[u][1]) + (v[u][2] + v[u][3]);
+    }
+    const float mu = sum16(s) * (1.f / C);
+    float ss = 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { const float d = v[u][j] - mu; ss += d * d; }
+    const float rs = rsqrtf(sum16(ss) * (1.f / C) + eps);
+    TO* yr = y + row * C + 4 * gl;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = (v[u][j] - mu) * rs * gg[u][j] + bb[u][j];
+      store4(yr + 64 * u, o);
+    }
+    if (gl == 0) { mean[row] = mu; rstd[row] = rs; }
+  }
+}
+
+// dx (+ dres) and per-block partial dgamma / dbeta (part_g/part_b [block][C]).
+template <typename TI, typename TD, int C>
+__global__ __launch_bounds__(256) void ln_bwd16_kernel(const TD* dy, const TI* x, const float* mean,
+                                                       const float* rstd, const float* g, TI* dx, float* part_g,
+                                                       float* part_b, int64_t M, int64_t rows_per_block,
+                                                       const TI* dres) {
+  constexpr int U = C / 64;
+  __shared__ float red[2][4][C];
+  const int gl = threadIdx.x & 15, grp = threadIdx.x >> 4, w = threadIdx.x >> 6;
+  float gw[U][4], ag[U][4], ab[U][4];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    load4(g + 64 * u + 4 * gl, gw[u]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { ag[u][j] = 0.f; ab[u][j] = 0.f; }
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
+  for (int64_t row = r0 + grp; row < r1; row += 16) {
+    const float mu = mean[row], rs = rstd[row];
+    const int64_t e0 = row * C + 4 * gl;
+    float xh[U][4], gy[U][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float xv[4], dv[4];
+      load4(x + e0 + 64 * u, xv);
+      load4(dy + e0 + 64 * u, dv);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        xh[u][j] = (xv[j] - mu) * rs;
+        gy[u][j] = dv[j] * gw[u][j];
+        s1 += gy[u][j];
+        s2 += gy[u][j] * xh[u][j];
+        ag[u][j] += dv[j] * xh[u][j];
+        ab[u][j] += dv[j];
+      }
+    }
+    s1 = sum16(s1) * (1.f / C);
+    s2 = sum16(s2) * (1.f / C);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = rs * (gy[u][j] - s1 - xh[u][j] * s2);
+      if (dres) {
+        float pr[4];
+        load4(dres + e0 + 64 * u, pr);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] += pr[j];
+      }
+      store4(dx + e0 + 64 * u, o);
+    }
+  }
+  // column partials: the 4 row groups of a wave, then the 4 waves (fixed order)
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float a = ag[u][j], c = ab[u][j];
+      a += __shfl_xor(a, 16, 64);
+      c += __shfl_xor(c, 16, 64);
+      a += __shfl_xor(a, 32, 64);
+      c += __shfl_xor(c, 32, 64);
+      ag[u][j] = a;
+      ab[u][j] = c;
+    }
+  if ((threadIdx.x & 63) < 16) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        red[0][w][64 * u + 4 * gl + j] = ag[u][j];
+        red[1][w][64 * u + 4 * gl + j] = ab[u][j];
+      }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    part_g[(int64_t)blockIdx.x * C + c] = (red[0][0][c] + red[0][1][c]) + (red[0][2][c] + red[0][3][c]);
+    part_b[(int64_t)blockIdx.x * C + c] = (red[1][0][c] + red[1][1][c]) + (red[1][2][c] + red[1][3][c]);
+  }
+}
+
 // ============================================================ BatchNorm (train)
 // Thread layout shared by the column-reduction kernels: thread t owns the 4-wide
 // channel chunk t % (C/4) and rows r = t / (C/4) (mod rows-per-pass).
@@ -513,6 +656,21 @@ extern "C" int sm_layernorm_fwd(int x_dtype, int y_dtype, int64_t M, int C, cons
                                 hipStream_t st) {
   if (M <= 0) return 0;
   if (C % 4 || C > 1024) return -2;
+  if (C == 384 || C == 192) {
+    int64_t rpb = ((M + 4095) / 4096 + 15) / 16 * 16;   // ~4096 blocks, 16-row multiples
+    if (rpb < 16) rpb = 16;
+    const int nb = (int)((M + rpb - 1) / rpb);
+    if (C == 384)
+      DISPATCH2(x_dtype, y_dtype,
+                hipLaunchKernelGGL((ln_fwd16_kernel<T1, T2, 384>), dim3(nb), dim3(256), 0, st, (const T1*)x, gamma,
+                                   beta, (T2*)y, mean, rstd, M, eps, rpb));
+    else
+      DISPATCH2(x_dtype, y_dtype,
+                hipLaunchKernelGGL((ln_fwd16_kernel<T1, T2, 192>), dim3(nb), dim3(256), 0, st, (const T1*)x, gamma,
+                                   beta, (T2*)y, mean, rstd, M, eps, rpb));
+    SM_CHECK_LAUNCH();
+    return 0;
+  }
   const int blocks = (int)((M + 3) / 4);
   DISPATCH2(x_dtype, y_dtype,
             hipLaunchKernelGGL((ln_fwd_kernel<T1, T2>), dim3(blocks), dim3(256), 0, st, (const T1*)x, gamma,
@@ -540,9 +698,18 @@ extern "C" int sm_layernorm_bwd(int x_dtype, int dy_dtype, int dx_dtype, int64_t
   float* pg = (float*)ws;
   float* pb = pg + (int64_t)nb * C;
   if (x_dtype != dx_dtype) return -3;   // dx has the dtype of the LN input stream
-  DISPATCH2(x_dtype, dy_dtype,
-            hipLaunchKernelGGL((ln_bwd_kernel<T1, T2, T1>), dim3(nb), dim3(256), 0, st, (const T2*)dy,
-                               (const T1*)x, mean, rstd, gamma, (T1*)dx, pg, pb, M, C, rpb, (const T1*)dres));
+  if (C == 384)
+    DISPATCH2(x_dtype, dy_dtype,
+              hipLaunchKernelGGL((ln_bwd16_kernel<T1, T2, 384>), dim3(nb), dim3(256), 0, st, (const T2*)dy,
+                                 (const T1*)x, mean, rstd, gamma, (T1*)dx, pg, pb, M, (int64_t)rpb, (const T1*)dres));
+  else if (C == 192)
+    DISPATCH2(x_dtype, dy_dtype,
+              hipLaunchKernelGGL((ln_bwd16_kernel<T1, T2, 192>), dim3(nb), dim3(256), 0, st, (const T2*)dy,
+                                 (const T1*)x, mean, rstd, gamma, (T1*)dx, pg, pb, M, (int64_t)rpb, (const T1*)dres));
+  else
+    DISPATCH2(x_dtype, dy_dtype,
+              hipLaunchKernelGGL((ln_bwd_kernel<T1, T2, T1>), dim3(nb), dim3(256), 0, st, (const T2*)dy,
+                                 (const T1*)x, mean, rstd, gamma, (T1*)dx, pg, pb, M, C, rpb, (const T1*)dres));
   SM_CHECK_LAUNCH();
   colred(pg, nb, C, nullptr, dgamma, 1, st);
   colred(pb, nb, C, nullptr, dbeta, 1, st);
