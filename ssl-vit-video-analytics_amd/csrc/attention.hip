@@ -126,6 +126,18 @@ SM_DEV bool attn_keep_byte(uint32_t h, int j, uint32_t thr) { return ((h >> (8 *
 SM_DEV uint32_t keep_flags(uint32_t h, uint32_t thr) { return (h & 0x7F7F7F7Fu) + (128u - thr) * 0x01010101u; }
 SM_DEV uint32_t keep_mask01(uint32_t y) { return __builtin_amdgcn_perm(y << 8, y, 0x08080A0Au); }   // bytes 0, 1
 SM_DEV uint32_t keep_mask23(uint32_t y) { return __builtin_amdgcn_perm(y << 8, y, 0x09090B0Bu); }   // bytes 2, 3
+// Per-element form for fp32 operands: keep_bytes() turns the four flags into bytes
+// 0xFF / 0x00 (one v_perm), and keep_sel() ANDs v with its byte sign-extended to 32
+// bits, which the compiler's SDWA peephole folds into one v_and_b32_sdwa (operand
+// select BYTE_j with sext) -- one instruction per element, where its lowering of
+// `keep ? v : 0` is byte extract + compare + select.  (Written in plain C so the
+// compiler still inserts the MFMA / transcendental read-after-write wait states an
+// inline-asm operand would not get.)
+SM_DEV uint32_t keep_bytes(uint32_t y) { return __builtin_amdgcn_perm(y << 8, y, 0x090B080Au); }
+SM_DEV float keep_sel(float v, uint32_t kb, int j) {
+  const uint32_t m = (uint32_t)(int32_t)(int8_t)(kb >> (8 * j));
+  return __uint_as_float(__float_as_uint(v) & m);
+}
 SM_DEV uint32_t pack_bf16x2(float lo, float hi) {
   typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
   const bf16x2 v = {(__bf16)lo, (__bf16)hi};
@@ -154,27 +166,31 @@ SM_DEV uint32_t quad_transpose_bytes(uint32_t v, uint32_t sel1, uint32_t sel2) {
 }
 
 // Per-thread plan for staging a [ROWS][D] bf16 tile (rows of a [L][ld] matrix) into
-// the LDS image: element offsets and LDS offsets are computed once; each tile is
-// then CH 16-byte loads issued early into registers (prefetch) and CH 16-byte
-// LDS stores after the barrier.
+// the LDS image: byte offsets and LDS offsets are computed once; each tile is then
+// CH 16-byte raw buffer loads issued early into registers (prefetch) and CH 16-byte
+// LDS stores after the barrier.  The tile's descriptor (scalar) carries the base
+// and num_records = valid rows x row bytes, so rows past L read as zero with no
+// per-lane address arithmetic, compare or branch in the tile loop.
 template <int D, int ROWS>
 struct Stager {
   static constexpr int CH = ROWS * D / 8 / 256;
-  int goff[CH], loff[CH], row[CH];
-  SM_DEV void init(int ld) {
+  uint32_t voff[CH];
+  int loff[CH], ld;
+  SM_DEV void init(int ld_) {
+    ld = ld_;
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
       const int c = threadIdx.x + 256 * i;
-      row[i] = c / (D / 8);
-      const int d = (c % (D / 8)) * 8;
-      goff[i] = row[i] * ld + d;
-      loff[i] = tile_off<D>(row[i], d);
+      const int row = c / (D / 8), d = (c % (D / 8)) * 8;
+      voff[i] = (uint32_t)(row * ld + d) * 2u;
+      loff[i] = tile_off<D>(row, d);
     }
   }
   SM_DEV void load(const __bf16* base, int rows_left, uint4 (&r)[CH]) const {
+    const int rows = rows_left < ROWS ? rows_left : ROWS;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, rows * ld * 2, 0x00020000);
 #pragma unroll
-    for (int i = 0; i < CH; ++i)
-      r[i] = row[i] < rows_left ? *(const uint4*)(base + goff[i]) : make_uint4(0, 0, 0, 0);
+    for (int i = 0; i < CH; ++i) r[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff[i], 0, 0));
   }
   SM_DEV void store(char* lds, const uint4 (&r)[CH]) const {
 #pragma unroll
@@ -457,8 +473,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(AttnArgs a) {
       }
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        uint32_t kb4 = 0;   // byte j: 7-bit keep byte of (query row 4g + j, this key)
-        if (DROP) kb4 = quad_transpose_bytes(mix24(dlb + (uint32_t)(q0 + 32 * u + 8 * g) * AG), sel1, sel2) & 0x7F7F7F7Fu;
+        uint32_t kb4 = 0;   // byte j: keep flag of (query row 4g + j, this key)
+        if (DROP)
+          kb4 = keep_bytes(keep_flags(quad_transpose_bytes(mix24(dlb + (uint32_t)(q0 + 32 * u + 8 * g) * AG), sel1, sel2), dthr));
         const float4 a4 = *(const float4*)&llse[32 * u + 8 * g + 4 * h];
         const float4 b4 = *(const float4*)&ldel[32 * u + 8 * g + 4 * h];
         const float lse4[4] = {a4.x, a4.y, a4.z, a4.w};
@@ -469,9 +486,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(AttnArgs a) {
           const float p = __builtin_amdgcn_exp2f(fmaf(sacc[r], c, -lse4[j]));
           const float dp = dpacc[r];
           if (DROP) {
-            const bool keep = ((kb4 >> (8 * j)) & 0xFFu) >= dthr;
-            sacc[r] = keep ? p : 0.f;                          // dropped P feeds dV (x ks at the end)
-            dpacc[r] = p * fmaf(keep ? dp : 0.f, ks, -del4[j]);   // dS
+            sacc[r] = keep_sel(p, kb4, j);                            // dropped P feeds dV (x ks at the end)
+            dpacc[r] = p * fmaf(keep_sel(dp, kb4, j), ks, -del4[j]);   // dS
           } else {
             sacc[r] = p;
             dpacc[r] = p * (dp - del4[j]);
@@ -587,13 +603,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16(AttnArgs a) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         uint32_t hv = 0;
-        if (DROP) hv = mix24(dlb + (uint32_t)((k0 >> 2) + 8 * u + 2 * g) * AC) & 0x7F7F7F7Fu;
+        if (DROP) hv = keep_bytes(keep_flags(mix24(dlb + (uint32_t)((k0 >> 2) + 8 * u + 2 * g) * AC), dthr));
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int r = 4 * g + j;
           const float p = __builtin_amdgcn_exp2f(fmaf(sacc[r], c, -lse2));
           const float dp = dpacc[r];
-          if (DROP) dpacc[r] = p * fmaf(((hv >> (8 * j)) & 0xFFu) >= dthr ? dp : 0.f, ks, -dl);
+          if (DROP) dpacc[r] = p * fmaf(keep_sel(dp, hv, j), ks, -dl);
           else dpacc[r] = p * (dp - dl);
         }
       }
