@@ -141,6 +141,14 @@ int sm_se_bwd(int dtype, const void* dy, const void* x, const float* act_mean, c
               void* dx, void* ws, int64_t ws_bytes, hipStream_t st);
 int sm_se_scale(int dtype, const void* x, const float* act_mean, const float* act_rstd, const float* act_w,
                 const float* act_b, int act_gelu, const float* s, void* y, int F, int HW, int C, hipStream_t st);
+/* Fused backward of SE(GELU(BN2(x))) -- sm_se_bwd followed by sm_bn_bwd(gelu) on its
+ * dx (tiny_vit.py:50-53), in two passes over (dy, x); dh2 is never materialised.
+ * dw / db accumulate BN2's weight / bias gradients. */
+int64_t sm_se_bn_bwd_workspace_bytes(int F, int HW, int C);
+int sm_se_bn_bwd(int dtype, const void* dy, const void* x, const float* bn_mean, const float* bn_rstd,
+                 const float* bn_w, const float* bn_b, int bn_gelu, int F, int HW, int C, int R, const float* w1,
+                 const float* w2, const float* s, const float* z1, float* dz2, float* dz1, void* dx, float* dw,
+                 float* db, void* ws, int64_t ws_bytes, hipStream_t st);
 
 /* ---- MAE glue: tube mask (mae_loader.py:80-90) + masked-token compaction
  * (train_ssl_mae.py:105), pos-embed/mask-token blend (mae_vit_adapter.py:97-104),

@@ -125,6 +125,9 @@ def mbconv(args):
     rep("se_bwd (act)", timeit(lambda: K.se_bwd(y, a, Fn, H * W, C, w1, w2, sg, h1, act=act), args.iters), 4)
     rep("bn_bwd gelu", timeit(lambda: K.bn_bwd(y, a, m, r, g, b, True, torch.zeros(C, device=dev),
                                                 torch.zeros(C, device=dev)), args.iters), 5)
+    z = torch.zeros(C, device=dev)
+    rep("se_bn_bwd (fused)", timeit(lambda: K.se_bn_bwd(y, a, Fn, H * W, C, w1, w2, sg, h1, act, z, z),
+                                    args.iters), 5)
 
 
 if __name__ == "__main__":

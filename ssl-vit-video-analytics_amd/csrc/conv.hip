@@ -339,16 +339,37 @@ struct DwRing {
   }
 };
 
+// Block -> (32-channel slice, frame) of the fused depthwise kernels.  1-D grid with
+// the bijective XCD remap (as the attention and GEMM kernels): the C/32 slices of a
+// frame -- 64-B pieces of the same 128-B lines of every pixel -- run back to back on
+// one XCD, so each line is fetched into (and written back from) one L2 once rather
+// than half-used by two XCDs.  remap = 0: plain order (A/B switch SM_DWF_REMAP=0).
+struct DwfBlock {
+  int cs;
+  int64_t f;
+  SM_DEV DwfBlock(int ncs, int remap) {
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    int v = bid;
+    if (remap) {
+      const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+      v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    }
+    cs = v % ncs;
+    f = v / ncs;
+  }
+};
+
 template <int S>
 __global__ __launch_bounds__(256, 2) void dwf_fwd_kernel(const __bf16* x, ChanAffine act, const float* w,
                                                          __bf16* y, float* part, int H, int W, int C, int Ho,
-                                                         int Wo) {
+                                                         int Wo, int remap) {
   using R = DwRing<S>;
   constexpr int TY = R::TY;
   constexpr int PX = DWF_PX;
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int cs = blockIdx.x;
-  const int64_t f = blockIdx.y;
+  const DwfBlock blk(C / DWF_CB, remap);
+  const int cs = blk.cs;
+  const int64_t f = blk.f;
   const int t = threadIdx.x;
   const int c8 = t & 3;
   const int cbase = cs * DWF_CB + c8 * 8;
@@ -447,13 +468,15 @@ __global__ __launch_bounds__(256, 2) void dwf_fwd_kernel(const __bf16* x, ChanAf
 // over the 64 threads that share its 8 channels: part[f][C][9] (colred over frames).
 template <int S>
 __global__ __launch_bounds__(256, 2) void dwf_wgrad_kernel(const __bf16* dy, const __bf16* x, ChanAffine act,
-                                                           float* part, int H, int W, int C, int Ho, int Wo) {
+                                                           float* part, int H, int W, int C, int Ho, int Wo,
+                                                           int remap) {
   using R = DwRing<S>;
   constexpr int TY = R::TY;
   constexpr int PX = DWF_PX;
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int cs = blockIdx.x;
-  const int64_t f = blockIdx.y;
+  const DwfBlock blk(C / DWF_CB, remap);
+  const int cs = blk.cs;
+  const int64_t f = blk.f;
   const int t = threadIdx.x;
   const int c8 = t & 3;
   const int cbase = cs * DWF_CB + c8 * 8;
@@ -746,6 +769,152 @@ __global__ __launch_bounds__(256) void se_fc_bwd_kernel(const float* part, int n
   }
 }
 
+// ------------------------------------------------------------------ fused SE + BN/GELU backward
+// MBConv's h2 = GELU(BN2(a2)), h3 = h2 * gate (tiny_vit.py:50-53): the backward of the
+// SE layer and of BN2 + GELU in two streaming passes over (dh3, a2) instead of four
+// (se_bwd: gate-gradient reduce + dh2 write; bn_bwd: reduce + dx), and dh2 never
+// exists in HBM.  dh2 = dh3 * s[f][c] + dpool[f][c] / HW is affine per (frame,
+// channel), so BN2's two channel sums over du = dh2 * GELU'(u) split into per-frame
+// sums of dh3 and of 1 that the frame's (s, dpool) weight once dpool is known:
+//   sum du      = sum_f (s * A_f + dpool/HW * B_f),  A = sum dh3 g',    B = sum g'
+//   sum du xhat = sum_f (s * X_f + dpool/HW * D_f),  X = sum dh3 g' xh, D = sum g' xh
+// Pass 1 (se_bn_reduce_kernel) produces the SE gate sums (se_reduce layout) and A, B,
+// X, D per (frame, split); pass 2 (se_bn_dx_kernel) recomputes dh2 and writes da2.
+struct BnCh8 {   // per-channel constants of the BatchNorm + GELU on 8 channels
+  float sc[8], sh[8], rs[8], mr[8], wr[8];
+  SM_DEV void init(const ChanAffine& a, int c0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + j;
+      rs[j] = a.rstd[c];
+      mr[j] = a.mean[c] * rs[j];
+      sc[j] = rs[j] * a.w[c];
+      sh[j] = a.b[c] - a.mean[c] * sc[j];
+      wr[j] = a.w[c] * rs[j];
+    }
+  }
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void se_bn_reduce_kernel(const T* dy, const T* x, ChanAffine act, int HW, int C,
+                                                           float* part /*[F][ns][C]*/,
+                                                           float* part2 /*[F][ns][4][C]*/) {
+  __shared__ float red[256 * 8];
+  const SeCols cm(C);
+  const int k = blockIdx.x, nsplit = gridDim.x;
+  const int64_t f = blockIdx.y;
+  const int p0 = k * SE_PX_PER_SPLIT, p1 = min(HW, p0 + SE_PX_PER_SPLIT);
+  float acc[5][8];
+#pragma unroll
+  for (int q = 0; q < 5; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[q][j] = 0.f;
+  if (cm.r < cm.rpp) {
+    BnCh8 bc;
+    bc.init(act, cm.c0);
+    for (int p = p0 + cm.r; p < p1; p += cm.rpp) {
+      const int64_t e = (f * HW + p) * C + cm.c0;
+      float v[8], g[8];
+      load8(x + e, v);
+      load8(dy + e, g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float xh = fmaf(v[j], bc.rs[j], -bc.mr[j]);
+        const float u = fmaf(v[j], bc.sc[j], bc.sh[j]);
+        float pdf;
+        const float cdf = gelu_phi_pair(u, &pdf);
+        const float h = to_f<T>(from_f<T>(u * cdf));   // the stored-precision SE input
+        const float gp = act.gelu ? fmaf(u, pdf, cdf) : 1.f;
+        const float hh = act.gelu ? h : to_f<T>(from_f<T>(u));
+        const float t = gp * xh;
+        acc[0][j] = fmaf(g[j], hh, acc[0][j]);
+        acc[1][j] = fmaf(g[j], gp, acc[1][j]);
+        acc[2][j] += gp;
+        acc[3][j] = fmaf(g[j], t, acc[3][j]);
+        acc[4][j] += t;
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    if (q) __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[threadIdx.x * 8 + j] = acc[q][j];
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += 256) {
+      float a = 0.f;
+      for (int rr = 0; rr < cm.rpp; ++rr) a += red[(rr * cm.nch + c / 8) * 8 + c % 8];
+      if (q == 0) part[(f * nsplit + k) * C + c] = a;
+      else part2[((f * nsplit + k) * 4 + (q - 1)) * C + c] = a;
+    }
+  }
+}
+
+// per frame: comb[f][0][c] = s A + dpool/HW B, comb[f][1][c] = s X + dpool/HW D
+__global__ __launch_bounds__(256) void se_bn_combine_kernel(const float* part2, int nsplit, int HW, int C,
+                                                            const float* s, const float* dpool, float* comb) {
+  const int64_t f = blockIdx.x;
+  const float inv = 1.f / (float)HW;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float q[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < nsplit; ++k)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) q[i] += part2[((f * nsplit + k) * 4 + i) * C + c];
+    const float sv = s[f * C + c], dp = dpool[f * C + c] * inv;
+    comb[(f * 2 + 0) * C + c] = sv * q[0] + dp * q[1];
+    comb[(f * 2 + 1) * C + c] = sv * q[2] + dp * q[3];
+  }
+}
+
+// sums [2][C] (fp64) -> dgamma (+=), dbeta (+=), coef [2][C] = mean(du), mean(du xhat)
+__global__ void se_bn_finalize_kernel(const double* sums, int64_t M, int C, float* dw, float* db, float* coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double a = sums[c], b = sums[C + c];
+  if (dw) dw[c] += (float)b;
+  if (db) db[c] += (float)a;
+  coef[c] = (float)(a / (double)M);
+  coef[C + c] = (float)(b / (double)M);
+}
+
+// da2 = w rstd (du - mean(du) - xhat mean(du xhat)),  du = (dh3 s + dpool/HW) GELU'(u)
+template <typename T>
+__global__ __launch_bounds__(256) void se_bn_dx_kernel(const T* dy, const T* x, ChanAffine act, const float* s,
+                                                       const float* dpool, const float* coef, T* dx, int HW,
+                                                       int C) {
+  const SeCols cm(C);
+  if (cm.r >= cm.rpp) return;
+  const int k = blockIdx.x;
+  const int64_t f = blockIdx.y;
+  const int p0 = k * SE_PX_PER_SPLIT, p1 = min(HW, p0 + SE_PX_PER_SPLIT);
+  BnCh8 bc;
+  bc.init(act, cm.c0);
+  float ss[8], ad[8], k0[8], k1[8];
+  const float inv = 1.f / (float)HW;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = cm.c0 + j;
+    ss[j] = s[f * C + c];
+    ad[j] = dpool[f * C + c] * inv;
+    k0[j] = coef[c];
+    k1[j] = coef[C + c];
+  }
+  for (int p = p0 + cm.r; p < p1; p += cm.rpp) {
+    const int64_t e = (f * HW + p) * C + cm.c0;
+    float v[8], g[8], o[8];
+    load8(x + e, v);
+    load8(dy + e, g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float xh = fmaf(v[j], bc.rs[j], -bc.mr[j]);
+      float du = fmaf(g[j], ss[j], ad[j]);
+      if (act.gelu) du *= gelu_grad(fmaf(v[j], bc.sc[j], bc.sh[j]));
+      o[j] = bc.wr[j] * (du - k0[j] - xh * k1[j]);
+    }
+    store8(dx + e, o);
+  }
+}
+
 }  // namespace
 
 #define DISPATCH1(DT, ...)                                       \
@@ -833,8 +1002,13 @@ static size_t dwf_lds_bytes(int W, int stride) {
   return lds < 256 * 16 * 4 ? 256 * 16 * 4 : lds;   // the statistics reduction reuses it
 }
 
+static int dwf_remap() {
+  static const int r = [] { const char* e = getenv("SM_DWF_REMAP"); return e ? atoi(e) : 1; }();
+  return r;
+}
+
 static bool dwf_shape_ok(int F, int W, int C, int stride) {
-  return C % DWF_CB == 0 && (stride == 1 || stride == 2) && F > 0 && F <= 65535 &&
+  return C % DWF_CB == 0 && (stride == 1 || stride == 2) && F > 0 && (int64_t)F * (C / DWF_CB) < (1LL << 31) &&
          DwRing<2>::NEW * W * 4 <= 256 * DWF_KV && DwRing<1>::NEW * W * 4 <= 256 * DWF_KV &&
          dwf_lds_bytes(W, stride) <= 64 * 1024;
 }
@@ -848,14 +1022,15 @@ extern "C" int sm_dwconv_fused_fwd(int F, int H, int W, int C, int stride, const
   if (((uintptr_t)w & 15) || ((uintptr_t)x & 15) || ((uintptr_t)y & 15)) return -2;
   const int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
   ChanAffine act{in_mean, in_rstd, in_w, in_b, in_gelu};
-  dim3 grid(C / DWF_CB, F);
+  const dim3 grid((C / DWF_CB) * F);
   const size_t lds = dwf_lds_bytes(W, stride);
+  const int remap = dwf_remap();
   if (stride == 1)
     hipLaunchKernelGGL((dwf_fwd_kernel<1>), grid, dim3(256), lds, st, (const __bf16*)x, act, w, (__bf16*)y, part,
-                       H, W, C, Ho, Wo);
+                       H, W, C, Ho, Wo, remap);
   else
     hipLaunchKernelGGL((dwf_fwd_kernel<2>), grid, dim3(256), lds, st, (const __bf16*)x, act, w, (__bf16*)y, part,
-                       H, W, C, Ho, Wo);
+                       H, W, C, Ho, Wo, remap);
   SM_CHECK_LAUNCH();
   return 0;
 }
@@ -886,8 +1061,8 @@ extern "C" int sm_dwconv_fused_bwd(int F, int H, int W, int C, int stride, const
     if (stride == 1) {
       hipLaunchKernelGGL(dw_rotate_kernel, dim3((C * 9 + 255) / 256), dim3(256), 0, st, w, wrot, C * 9);
       ChanAffine none{nullptr, nullptr, nullptr, nullptr, 0};
-      hipLaunchKernelGGL((dwf_fwd_kernel<1>), dim3(C / DWF_CB, F), dim3(256), lds, st, (const __bf16*)dy, none,
-                         (const float*)wrot, (__bf16*)dx, (float*)nullptr, Ho, Wo, C, H, W);
+      hipLaunchKernelGGL((dwf_fwd_kernel<1>), dim3((C / DWF_CB) * F), dim3(256), lds, st, (const __bf16*)dy, none,
+                         (const float*)wrot, (__bf16*)dx, (float*)nullptr, Ho, Wo, C, H, W, dwf_remap());
     } else {
       const int64_t total = (int64_t)F * H * ((W + DW_PX - 1) / DW_PX) * (C / 8);
       hipLaunchKernelGGL((dw_dgrad_kernel<__bf16, 2>), dim3((int)((total + 255) / 256)), dim3(256), 0, st,
@@ -895,13 +1070,13 @@ extern "C" int sm_dwconv_fused_bwd(int F, int H, int W, int C, int stride, const
     }
   }
   ChanAffine act{in_mean, in_rstd, in_w, in_b, in_gelu};
-  dim3 g2(C / DWF_CB, F);
+  const dim3 g2((C / DWF_CB) * F);
   if (stride == 1)
     hipLaunchKernelGGL((dwf_wgrad_kernel<1>), g2, dim3(256), lds, st, (const __bf16*)dy, (const __bf16*)x, act, part,
-                       H, W, C, Ho, Wo);
+                       H, W, C, Ho, Wo, dwf_remap());
   else
     hipLaunchKernelGGL((dwf_wgrad_kernel<2>), g2, dim3(256), lds, st, (const __bf16*)dy, (const __bf16*)x, act, part,
-                       H, W, C, Ho, Wo);
+                       H, W, C, Ho, Wo, dwf_remap());
   colred(part, F, C * 9, nullptr, dw, 1, st);
   SM_CHECK_LAUNCH();
   return 0;
@@ -1001,6 +1176,42 @@ extern "C" int sm_se_scale(int dtype, const void* x, const float* act_mean, cons
   ChanAffine act{act_mean, act_rstd, act_w, act_b, act_gelu};
   DISPATCH1(dtype, hipLaunchKernelGGL(se_apply_kernel<T>, dim3(se_splits(HW), F), dim3(256), 0, st, (const T*)x,
                                       act, s, (const float*)nullptr, (T*)y, HW, C));
+  SM_CHECK_LAUNCH();
+  return 0;
+}
+
+// Fused backward of h3 = SE(h2), h2 = GELU(BN2(x)) (batch statistics mean/rstd of x
+// over M = F*HW rows): dx = dL/dx, dz2 / dz1 as sm_se_bwd, dgamma / dbeta += (dw, db).
+extern "C" int64_t sm_se_bn_bwd_workspace_bytes(int F, int HW, int C) {
+  const int64_t ns = se_splits(HW);
+  return (F * ns * C + (int64_t)F * C + F * ns * 4 * C + (int64_t)F * 2 * C + 2 * C) * 4 + 2 * C * 8 + 64;
+}
+
+extern "C" int sm_se_bn_bwd(int dtype, const void* dy, const void* x, const float* bn_mean, const float* bn_rstd,
+                            const float* bn_w, const float* bn_b, int bn_gelu, int F, int HW, int C, int R,
+                            const float* w1, const float* w2, const float* s, const float* z1, float* dz2,
+                            float* dz1, void* dx, float* dw, float* db, void* ws, int64_t ws_bytes,
+                            hipStream_t st) {
+  if (C % 8 || C / 8 > 256 || F <= 0 || F > 65535 || HW <= 0 || !bn_mean) return -2;
+  if (ws_bytes < sm_se_bn_bwd_workspace_bytes(F, HW, C)) return -4;
+  const int ns = se_splits(HW);
+  float* part = (float*)ws;
+  float* dpool = part + (int64_t)F * ns * C;
+  float* part2 = dpool + (int64_t)F * C;
+  float* comb = part2 + (int64_t)F * ns * 4 * C;
+  float* coef = comb + (int64_t)F * 2 * C;
+  double* sums = (double*)(((uintptr_t)(coef + 2 * C) + 7) & ~(uintptr_t)7);
+  ChanAffine act{bn_mean, bn_rstd, bn_w, bn_b, bn_gelu};
+  DISPATCH1(dtype, hipLaunchKernelGGL(se_bn_reduce_kernel<T>, dim3(ns, F), dim3(256), 0, st, (const T*)dy,
+                                      (const T*)x, act, HW, C, part, part2));
+  hipLaunchKernelGGL(se_fc_bwd_kernel, dim3(F), dim3(256), (C + R) * 4, st, part, ns, s, z1, w1, w2, C, R, dz2, dz1,
+                     dpool);
+  hipLaunchKernelGGL(se_bn_combine_kernel, dim3(F), dim3(256), 0, st, part2, ns, HW, C, s, dpool, comb);
+  colred(comb, F, 2 * C, sums, nullptr, 0, st);
+  hipLaunchKernelGGL(se_bn_finalize_kernel, dim3((C + 127) / 128), dim3(128), 0, st, sums, (int64_t)F * HW, C, dw,
+                     db, coef);
+  DISPATCH1(dtype, hipLaunchKernelGGL(se_bn_dx_kernel<T>, dim3(ns, F), dim3(256), 0, st, (const T*)dy, (const T*)x,
+                                      act, s, dpool, coef, (T*)dx, HW, C));
   SM_CHECK_LAUNCH();
   return 0;
 }

@@ -61,6 +61,8 @@ _SIGS = {
     "sm_se_fwd": (_c_i32, [_c_i32, _c_p] + [_c_p] * 4 + [_c_i32] * 5 + [_c_p] * 7 + [_c_i64, _c_p]),
     "sm_se_bwd": (_c_i32, [_c_i32, _c_p, _c_p] + [_c_p] * 4 + [_c_i32] * 5 + [_c_p] * 8 + [_c_i64, _c_p]),
     "sm_se_scale": (_c_i32, [_c_i32, _c_p] + [_c_p] * 4 + [_c_i32, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_p]),
+    "sm_se_bn_bwd_workspace_bytes": (_c_i64, [_c_i32, _c_i32, _c_i32]),
+    "sm_se_bn_bwd": (_c_i32, [_c_i32, _c_p, _c_p] + [_c_p] * 4 + [_c_i32] * 5 + [_c_p] * 9 + [_c_p, _c_i64, _c_p]),
     "sm_dwconv_fused_partial_rows": (_c_i64, [_c_i32, _c_i32, _c_i32]),
     "sm_dwconv_fused_fwd": (_c_i32, [_c_i32] * 5 + [_c_p] * 5 + [_c_i32] + [_c_p] * 4),
     "sm_dwconv_fused_bwd_workspace_bytes": (_c_i64, [_c_i32] * 5),

@@ -201,16 +201,18 @@ class MBConvFn(torch.autograd.Function):
         dh3 = K.linear_dx(da3, W(w_proj, mode).view(Cout, mid))
         del da3
         if ctx.fused:
-            dh2, dz2, dz1 = K.se_bwd(dh3, a2, Fr, Ho * Wo, mid, w_fc0.detach(), w_fc2.detach(), gate, h1se, act=act2)
+            # SE backward + BN2/GELU backward in two passes over (dh3, a2); no dh2 in HBM
+            da2, dz2, dz1 = K.se_bn_bwd(dh3, a2, Fr, Ho * Wo, mid, w_fc0.detach(), w_fc2.detach(), gate, h1se,
+                                        act2, G(g2), G(b2))
         else:
             dh2, dz2, dz1 = K.se_bwd(dh3, h2, Fr, Ho * Wo, mid, w_fc0.detach(), w_fc2.detach(), gate, h1se)
             del h2
+            da2 = K.bn_bwd(dh2, a2, m2, r2, g2.detach(), b2.detach(), True, G(g2), G(b2))
+            del dh2
         del dh3
         R = mid // 4
         K.gemm(dz2, h1se, G(w_fc2), mid, R, Fr, 1, 1, mid, R, R, beta=1.0)
         K.gemm(dz1, pooled, G(w_fc0), R, mid, Fr, 1, 1, R, mid, mid, beta=1.0)
-        da2 = K.bn_bwd(dh2, a2, m2, r2, g2.detach(), b2.detach(), True, G(g2), G(b2))
-        del dh2
         if a1 is None:
             a1 = K.linear(x.reshape(-1, Cin), W(w_exp, mode).view(mid, Cin))
         if ctx.fused:

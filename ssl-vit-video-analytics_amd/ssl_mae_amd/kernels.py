@@ -341,6 +341,23 @@ def se_bwd(dy, x, F, HW, C, w1, w2, s, h1, act=None):
     return dx, dz2, dz1
 
 
+def se_bn_bwd(dy, x, F, HW, C, w1, w2, s, h1, act, dw_sink, db_sink):
+    """Fused backward of y = SE(GELU(BN(x))) with BN's batch statistics act = (mean,
+    rstd, w, b, gelu): returns (dx, dz2, dz1) as se_bwd followed by bn_bwd on its dx;
+    dw_sink / db_sink accumulate BN's weight / bias gradients."""
+    _chk(dy, x)
+    R = w1.shape[0]
+    dev = x.device
+    dz2 = torch.empty((F, C), dtype=torch.float32, device=dev)
+    dz1 = torch.empty((F, R), dtype=torch.float32, device=dev)
+    dx = torch.empty_like(x)
+    nbytes = query("sm_se_bn_bwd_workspace_bytes", F, HW, C)
+    ws = _ws(nbytes, dev)
+    call("sm_se_bn_bwd", dt(x), ptr(dy), ptr(x), *_act_args(act), F, HW, C, R, ptr(w1), ptr(w2), ptr(s), ptr(h1),
+         ptr(dz2), ptr(dz1), ptr(dx), ptr(dw_sink), ptr(db_sink), ptr(ws), nbytes, stream())
+    return dx, dz2, dz1
+
+
 # ------------------------------------------------------------------ MAE glue
 def tube_mask(noise, T, n_mask, with_index=True):
     """noise [B,L] fp32 (device) -> mask uint8 [B,T,L], idx int32 [B*T*n_mask]."""

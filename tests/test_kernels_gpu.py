@@ -412,6 +412,28 @@ def test_se_fused_act_matches_materialised(HW, C):
     assert rel_err(dx, dx_r) < 1e-2
 
 
+@pytest.mark.parametrize("HW,C", [(49, 96), (1000, 384)])
+def test_se_bn_bwd_fused_matches_composition(HW, C):
+    """Fused SE + BN2/GELU backward == se_bwd followed by bn_bwd(gelu) on its dx
+    (the composed path rounds dh2 to bf16 in HBM; the fused one keeps it in fp32)."""
+    kk = KK()
+    Fn, R = 3, C // 4
+    a = (rnd(Fn * HW, C, seed=105) * 2).to(torch.bfloat16).to(DEV)
+    act = _act_for(a, 106)
+    w1 = (rnd(R, C, seed=107) * 0.2).to(DEV)
+    w2 = (rnd(C, R, seed=108) * 0.2).to(DEV)
+    _, _, h1, s = kk.se_fwd(a, Fn, HW, C, w1, w2, act=act)
+    dy = rnd(Fn * HW, C, seed=109).to(torch.bfloat16).to(DEV)
+    dh2, dz2_r, dz1_r = kk.se_bwd(dy, a, Fn, HW, C, w1, w2, s, h1, act=act)
+    dw_r, db_r = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    dx_r = kk.bn_bwd(dh2, a, act[0], act[1], act[2], act[3], True, dw_r, db_r)
+    dw, db = torch.full((C,), 0.5, device=DEV), torch.full((C,), -0.5, device=DEV)
+    dx, dz2, dz1 = kk.se_bn_bwd(dy, a, Fn, HW, C, w1, w2, s, h1, act, dw, db)
+    assert rel_err(dz2, dz2_r) < 1e-5 and rel_err(dz1, dz1_r) < 1e-5
+    assert rel_err(dw - 0.5, dw_r) < 5e-3 and rel_err(db + 0.5, db_r) < 5e-3
+    assert rel_err(dx, dx_r) < 1e-2
+
+
 # ------------------------------------------------------------------ MAE glue
 def test_tube_mask_and_gather_bit_exact():
     from oracle import mae_oracle as O
