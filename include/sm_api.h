@@ -40,6 +40,13 @@ int sm_gemm(int ab_dtype, int c_dtype, int a_layout, int b_layout, int M, int N,
             const float* bias, float alpha, float beta, int epi, void* aux, const void* R,
             float drop_p, uint64_t seed, const float* row_scale, int64_t rows_per_group,
             void* workspace, int64_t ws_bytes, hipStream_t stream);
+/* Weight + bias gradient of y = x W^T + b (Linear / 1x1 conv backward, e.g.
+ * tiny_vit.py:74-84 Mlp, mae_vit_adapter.py:40-48 decoder layers): dW[nout][nin]
+ * (+)= dy^T x and db[nout] += sum_rows dy in one GEMM pass over dy (bf16 dy, x;
+ * fp32 dW, db).  Replaces sm_gemm (dW) followed by sm_colsum (db). */
+int64_t sm_linear_dw_bias_workspace_bytes(int rows, int nout, int nin);
+int sm_linear_dw_bias(int rows, int nout, int nin, const void* dy, const void* x, float* dW, float* db,
+                      int accumulate, void* ws, int64_t ws_bytes, hipStream_t stream);
 
 /* ---- fused attention (tiny_vit.py:103 F.scaled_dot_product_attention;
  * torch MultiheadAttention core of the decoder, mae_vit_adapter.py:40-48).

@@ -543,18 +543,27 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16(AttnArgs a) {
   const int q = tl.qb * 128 + w * 32 + (l & 31);
   const bool qok = q < a.L;
   const float lse2 = qok ? a.lse[((int64_t)n * a.H + hd) * a.L + q] * LOG2E : 1e30f;
-  const float dl = qok ? a.delta[((int64_t)n * a.H + hd) * a.L + q] : 0.f;
 
+  // This lane's half of dO's and O's row for query q (D/2 values): Delta = rowsum(dO*O)
+  // is formed here (the two halves combined by a lane-32 swap) and written for the
+  // dK/dV kernel, which runs after this one -- no separate Delta pass over O and dO.
+  const __bf16* ob = (const __bf16*)a.o + (int64_t)n * a.L * C + hd * D;
   bf16x8 qf[D / 16], df[D / 16];
+  float dpart = 0.f;
 #pragma unroll
   for (int s = 0; s < D / 16; ++s) {
     if (qok) {
       qf[s] = *(const bf16x8*)(qb + (int64_t)q * ldq + 16 * s + 8 * h);
       df[s] = *(const bf16x8*)(dob + (int64_t)q * C + 16 * s + 8 * h);
+      const bf16x8 of = *(const bf16x8*)(ob + (int64_t)q * C + 16 * s + 8 * h);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dpart = fmaf((float)df[s][j], (float)of[j], dpart);
     } else {
       for (int j = 0; j < 8; ++j) { qf[s][j] = (__bf16)0.f; df[s][j] = (__bf16)0.f; }
     }
   }
+  const float dl = halves_sum(dpart);
+  if (qok && h == 0) a.delta[((int64_t)n * a.H + hd) * a.L + q] = dl;
   Stager<D, KT> stg;
   stg.init(ldq);
   int roff[D / 16], tlo[D / 32], thi[D / 32];
@@ -808,22 +817,20 @@ extern "C" int sm_attn_bwd(int dtype, int N, int L, int H, int D, const void* qk
   AttnArgs a{};
   a.qkv = qkv; a.o = o; a.dout = dout; a.lse = (float*)lse; a.delta = delta_ws; a.out = dqkv;
   a.N = N; a.L = L; a.H = H; a.scale = scale; a.drop_p = drop_p; a.seed = seed;
-  const int64_t rows = (int64_t)N * L;
-  const int dblocks = (int)((rows + 3) / 4);
-  if (dtype == SM_BF16) hipLaunchKernelGGL(attn_delta_kernel<__bf16>, dim3(dblocks), dim3(256), 0, st, a, D);
-  else hipLaunchKernelGGL(attn_delta_kernel<float>, dim3(dblocks), dim3(256), 0, st, a, D);
-  SM_CHECK_LAUNCH();
   dim3 grid((L + 127) / 128, H, N);
   const dim3 grid1((unsigned)(((L + 127) / 128) * H * N));   // bf16 kernels: 1-D, XCD-remapped
   const bool drop = drop_p > 0.f;
   if (dtype == SM_BF16) {
+    // dQ first: it forms Delta = rowsum(dO*O) in its prologue for the dK/dV kernel
 #define SM_ATTN_BWD(DD, DR)                                                        \
-  hipLaunchKernelGGL((attn_bwd_dkdv_bf16<DD, DR>), grid1, dim3(256), 0, st, a);    \
-  hipLaunchKernelGGL((attn_bwd_dq_bf16<DD, DR>), grid1, dim3(256), 0, st, a);
+  hipLaunchKernelGGL((attn_bwd_dq_bf16<DD, DR>), grid1, dim3(256), 0, st, a);      \
+  hipLaunchKernelGGL((attn_bwd_dkdv_bf16<DD, DR>), grid1, dim3(256), 0, st, a);
     if (D == 32) { if (drop) { SM_ATTN_BWD(32, true) } else { SM_ATTN_BWD(32, false) } }
     else { if (drop) { SM_ATTN_BWD(64, true) } else { SM_ATTN_BWD(64, false) } }
 #undef SM_ATTN_BWD
   } else {
+    const int dblocks = (int)(((int64_t)N * L + 3) / 4);
+    hipLaunchKernelGGL(attn_delta_kernel<float>, dim3(dblocks), dim3(256), 0, st, a, D);
     if (D == 32) {
       hipLaunchKernelGGL(attn_bwd_dkdv_f32<32>, grid, dim3(128), 0, st, a);
       hipLaunchKernelGGL(attn_bwd_dq_f32<32>, grid, dim3(128), 0, st, a);

@@ -40,6 +40,7 @@ struct GemmArgs {
   const float* row_scale;   // DropPath: branch *= row_scale[row / rows_per_group]
   int64_t rows_per_group;
   float* partial;   // split-K fp32 slabs [z][M][N] (when non-null: raw store, no epilogue)
+  float* colsum;    // bf16 v2, M/N-contiguous A only: per-split row sums of A, [z][M]
 };
 
 template <typename TC>
@@ -526,7 +527,22 @@ __global__ __launch_bounds__(BMV * 2, BMV == 256 ? 4 : 2) void gemm_bf16_v2(Gemm
     tla.load(panel_rsrc(A, abase + kb * astep), ke - kb, ra);
     tlb.load(panel_rsrc(B, bbase + kb * bstep), ke - kb, rb);
   }
+  // Bias gradient of a weight-gradient GEMM (A = dy^T, M/N-contiguous): the n0 == 0
+  // block of each m-tile also sums its A chunks over K (8 rows of M per thread, from
+  // the staging registers), so db needs no separate pass over dy.
+  const bool csum = !AK && g.colsum != nullptr && n0 == 0;
+  float cs8[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) cs8[j] = 0.f;
   for (int k0 = kb; k0 < ke; k0 += BKT) {
+    if (csum) {
+#pragma unroll
+      for (int i = 0; i < TileLoader<BMV, NT, AK>::CH; ++i) {
+        const bf16x8 v = __builtin_bit_cast(bf16x8, ra[i]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cs8[j] += (float)v[j];
+      }
+    }
     tla.store(la, ra);
     tlb.store(lb, rb);
     __syncthreads();
@@ -546,6 +562,20 @@ __global__ __launch_bounds__(BMV * 2, BMV == 256 ? 4 : 2) void gemm_bf16_v2(Gemm
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  if (csum) {   // block-uniform: reduce the NT / (BMV / 8) threads that share 8 rows
+    constexpr int G = BMV / 8;
+    float* red = (float*)lds;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[threadIdx.x * 8 + j] = cs8[j];
+    __syncthreads();
+    if ((int)threadIdx.x < BMV) {
+      const int c = threadIdx.x, cg = c >> 3, j = c & 7;
+      float sum = 0.f;
+      for (int q = 0; q < NT / G; ++q) sum += red[(q * G + cg) * 8 + j];
+      if (m0 + c < g.M) g.colsum[(int64_t)blockIdx.z * g.M + m0 + c] = sum;
     }
     __syncthreads();
   }
@@ -702,11 +732,11 @@ extern "C" int64_t sm_gemm_workspace_bytes(int ab_dtype, int M, int N, int K) {
   return s > 1 ? (int64_t)s * M * N * 4 : 0;
 }
 
-extern "C" int sm_gemm(int ab_dtype, int c_dtype, int a_layout, int b_layout, int M, int N, int K,
-                       const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc,
-                       const float* bias, float alpha, float beta, int epi, void* aux, const void* R,
-                       float drop_p, uint64_t seed, const float* row_scale, int64_t rows_per_group,
-                       void* workspace, int64_t ws_bytes, hipStream_t stream) {
+static int gemm_run(int ab_dtype, int c_dtype, int a_layout, int b_layout, int M, int N, int K, const void* A,
+                    int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, const float* bias, float alpha,
+                    float beta, int epi, void* aux, const void* R, float drop_p, uint64_t seed,
+                    const float* row_scale, int64_t rows_per_group, void* workspace, int64_t ws_bytes,
+                    float* colsum, float* colsum_out, hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
   if (ab_dtype == SM_BF16) {
     if (K % 8 || lda % 8 || ldb % 8) return -2;
@@ -718,6 +748,7 @@ extern "C" int sm_gemm(int ab_dtype, int c_dtype, int a_layout, int b_layout, in
   g.M = M; g.N = N; g.K = K; g.A = A; g.lda = lda; g.B = B; g.ldb = ldb; g.C = C; g.ldc = ldc;
   g.bias = bias; g.alpha = alpha; g.beta = beta; g.epi = epi; g.aux = aux; g.R = R;
   g.drop_p = drop_p; g.seed = seed; g.row_scale = row_scale; g.rows_per_group = rows_per_group > 0 ? rows_per_group : 1;
+  g.colsum = colsum;
   int splits = choose_splits(M, N, K, ab_dtype == SM_BF16);
   if (splits > 1 && (workspace == nullptr || ws_bytes < (int64_t)splits * M * N * 4)) splits = 1;
   const int bk = ab_dtype == SM_BF16 ? BKT : FBK;
@@ -745,5 +776,38 @@ extern "C" int sm_gemm(int ab_dtype, int c_dtype, int a_layout, int b_layout, in
     else hipLaunchKernelGGL(splitk_reduce_kernel<float>, dim3(blocks), dim3(256), 0, stream, g, splits);
     SM_CHECK_LAUNCH();
   }
+  if (colsum) {
+    colred(colsum, K > 0 ? splits : 0, M, nullptr, colsum_out, 1, stream);
+    SM_CHECK_LAUNCH();
+  }
   return 0;
+}
+
+extern "C" int sm_gemm(int ab_dtype, int c_dtype, int a_layout, int b_layout, int M, int N, int K,
+                       const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc,
+                       const float* bias, float alpha, float beta, int epi, void* aux, const void* R,
+                       float drop_p, uint64_t seed, const float* row_scale, int64_t rows_per_group,
+                       void* workspace, int64_t ws_bytes, hipStream_t stream) {
+  return gemm_run(ab_dtype, c_dtype, a_layout, b_layout, M, N, K, A, lda, B, ldb, C, ldc, bias, alpha, beta, epi,
+                  aux, R, drop_p, seed, row_scale, rows_per_group, workspace, ws_bytes, nullptr, nullptr, stream);
+}
+
+// Weight and bias gradients of y = x W^T + b in one pass over dy: dW[nout][nin] (+)=
+// dy^T x and db[nout] += column sums of dy (reference: the Linear / 1x1-conv
+// backward autograd runs as two ops, a GEMM and a sum over rows).  bf16 operands.
+extern "C" int64_t sm_linear_dw_bias_workspace_bytes(int rows, int nout, int nin) {
+  const int s = choose_splits(nout, nin, rows, true);
+  return (s > 1 ? (int64_t)s * nout * nin * 4 : 0) + (int64_t)s * nout * 4 + 256;
+}
+
+extern "C" int sm_linear_dw_bias(int rows, int nout, int nin, const void* dy, const void* x, float* dW, float* db,
+                                 int accumulate, void* ws, int64_t ws_bytes, hipStream_t stream) {
+  if (nout <= 0 || nin <= 0) return 0;
+  if (ws_bytes < sm_linear_dw_bias_workspace_bytes(rows, nout, nin)) return -4;
+  if (gemm_variant(nout, nin) == 1 || nout % 8 || nin % 8) return -2;   // the row sums live in the v2 kernel
+  const int s = choose_splits(nout, nin, rows, true);
+  const int64_t gbytes = s > 1 ? (int64_t)s * nout * nin * 4 : 0;
+  float* colsum = (float*)(((uintptr_t)ws + gbytes + 15) & ~(uintptr_t)15);
+  return gemm_run(SM_BF16, SM_F32, 1, 1, nout, nin, rows, dy, nout, x, nin, dW, nin, nullptr, 1.f,
+                  accumulate ? 1.f : 0.f, 0, nullptr, nullptr, 0.f, 0, nullptr, 1, ws, gbytes, colsum, db, stream);
 }

@@ -279,16 +279,14 @@ class BlockFn(torch.autograd.Function):
         if st.drop2 > 0 or st.dp2 is not None:
             db = K.dropout_bwd(db, st.drop2, st.seed2, st.dp2, L)
         h = K.gelu(hpre, st.drop_ff, st.seed_ff)
-        K.linear_dw(db, h, G(w2))
-        K.colsum(db, G(b2))
+        K.linear_dw_bias(db, h, G(w2), G(b2))
         del h
         dh = K.linear_dx(db, W(w2, mode))
         del db
         dhpre = K.gelu_bwd(hpre, dh, st.drop_ff, st.seed_ff)
         del dh
         ln2 = K.layernorm(x2, ln2w.detach(), ln2b.detach(), out_dtype=act, eps=st.eps)[0]
-        K.linear_dw(dhpre, ln2, G(w1))
-        K.colsum(dhpre, G(b1))
+        K.linear_dw_bias(dhpre, ln2, G(w1), G(b1))
         del ln2
         dln2 = K.linear_dx(dhpre, W(w1, mode))
         del dhpre
@@ -297,15 +295,13 @@ class BlockFn(torch.autograd.Function):
         dxb = dx2 if dx2.dtype == act else K.cast(dx2, act)
         if st.drop1 > 0 or st.dp1 is not None:
             dxb = K.dropout_bwd(dxb, st.drop1, st.seed1, st.dp1, L)
-        K.linear_dw(dxb, o, G(wproj))
-        K.colsum(dxb, G(bproj))
+        K.linear_dw_bias(dxb, o, G(wproj), G(bproj))
         do = K.linear_dx(dxb, W(wproj, mode))
         del dxb
         dqkv = K.attn_bwd(qkv, o, do, lse, N, L, H, D, st.attn_drop, st.seed_attn)
         del do
         ln1 = K.layernorm(x, ln1w.detach(), ln1b.detach(), out_dtype=act, eps=st.eps)[0]
-        K.linear_dw(dqkv, ln1, G(wqkv))
-        K.colsum(dqkv, G(bqkv))
+        K.linear_dw_bias(dqkv, ln1, G(wqkv), G(bqkv))
         del ln1
         dln1 = K.linear_dx(dqkv, W(wqkv, mode))
         del dqkv
@@ -341,8 +337,7 @@ class EncToDecFn(torch.autograd.Function):
         dx = dx.float().contiguous()
         dy = K.pos_blend_bwd(dx, mask_u8, mode.act, G(tpos).reshape(-1, D), G(spos).reshape(L, D),
                              G(tok).reshape(D), B, T, L, D)
-        K.linear_dw(dy, lat, G(w))
-        K.colsum(dy, G(b))
+        K.linear_dw_bias(dy, lat, G(w), G(b))
         dlat = K.linear_dx(dy, W(w, mode))
         return dlat, None, None, None, None, None, None, None
 
@@ -369,8 +364,7 @@ class HeadFn(torch.autograd.Function):
         _touch(*ctx.params)
         dpred = dpred.to(mode.act).contiguous()
         ln = K.layernorm(x, lnw.detach(), lnb.detach(), out_dtype=mode.act)[0]
-        K.linear_dw(dpred, ln, G(w))
-        K.colsum(dpred, G(b))
+        K.linear_dw_bias(dpred, ln, G(w), G(b))
         del ln
         dln = K.linear_dx(dpred, W(w, mode))
         dx = K.layernorm_bwd(dln, x, mu, rs, lnw.detach(), G(lnw), G(lnb))

@@ -68,6 +68,22 @@ def linear_dw(dy, x, grad_sink, accumulate=True):
     return grad_sink
 
 
+def linear_dw_bias(dy, x, grad_w, grad_b):
+    """grad_w[N,K] += dy^T @ x and grad_b[N] += sum over rows of dy.  bf16: one GEMM
+    whose n0 == 0 blocks also sum dy (sm_linear_dw_bias); fp32 (parity): two ops."""
+    M, N = dy.shape
+    K = x.shape[1]
+    if dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and M % 8 == 0 and N % 8 == 0 and K % 8 == 0:
+        _chk(dy, x, grad_w, grad_b)
+        nbytes = query("sm_linear_dw_bias_workspace_bytes", M, N, K)
+        ws = _ws(nbytes, dy.device)
+        call("sm_linear_dw_bias", M, N, K, ptr(dy), ptr(x), ptr(grad_w), ptr(grad_b), 1, ptr(ws), nbytes, stream())
+        return grad_w
+    linear_dw(dy, x, grad_w)
+    colsum(dy, grad_b)
+    return grad_w
+
+
 def colsum(x, out, accumulate=True):
     M, C = x.shape
     nbytes = query("sm_colsum_workspace_bytes", M, C)

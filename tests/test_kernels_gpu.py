@@ -96,6 +96,19 @@ def test_gemm_splitk_dw(dtype):
     assert rel_err(sink, ref) < (1e-4 if dtype == torch.float32 else 2e-2)
 
 
+@pytest.mark.parametrize("M,N,Kd", [(70000, 96, 384), (70000, 384, 1536), (1000, 200, 64), (344, 1152, 384)])
+def test_linear_dw_bias_fused(M, N, Kd):
+    """dW (+)= dy^T x with db += colsum(dy) from the same GEMM (bf16), split-K and
+    single-pass shapes, ragged M-tiles (N = 200: 256-row tile, 56 rows out of range)."""
+    dy = rnd(M, N, dtype=torch.bfloat16, seed=14, scale=0.1)
+    x = rnd(M, Kd, dtype=torch.bfloat16, seed=15)
+    gw = torch.full((N, Kd), 0.25, device=DEV)
+    gb = torch.full((N,), -0.5, device=DEV)
+    KK().linear_dw_bias(dy.to(DEV), x.to(DEV), gw, gb)
+    assert rel_err(gw - 0.25, dy.float().t() @ x.float()) < 2e-2
+    assert rel_err(gb + 0.5, dy.float().sum(0)) < 1e-4
+
+
 def test_colsum():
     x = rnd(5000, 384, seed=13)
     out = torch.ones(384, device=DEV)
