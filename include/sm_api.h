@@ -191,6 +191,20 @@ int sm_adamw(float* p, const float* g, float* m, float* v, void* bf16_shadow, in
              float b1, float b2, float eps, float wd, const int* found_inf, int64_t* step,
              int advance_step, hipStream_t st);
 
+/* ---- federated averaging (src/federated/fed_loop.py:14-62 fedavg_aggregate).
+ * out[i] = sum_j client_bufs[j][i] * weights[j], accumulated from +0 in client order
+ * with the product and the sum rounded separately (fed_loop.py:46-49, weights[j] =
+ * fp32(w_j / total_w)): bit-identical to the reference's CPU loop.  client_bufs is a
+ * HOST array of num_clients device pointers (1 <= num_clients <= SM_FEDAVG_MAX_CLIENTS),
+ * each holding one client's floating-point state_dict entries flattened in key order.
+ * sm_fedavg_counters_max: out[i] = max_j client_counters[j][i] (num_batches_tracked,
+ * fed_loop.py:52-55). */
+#define SM_FEDAVG_MAX_CLIENTS 32
+int sm_fedavg_weighted_sum(int num_clients, const float* const* client_bufs, const float* weights, int64_t n,
+                           float* out, hipStream_t st);
+int sm_fedavg_counters_max(int num_clients, const int64_t* const* client_counters, int64_t n, int64_t* out,
+                           hipStream_t st);
+
 #ifdef __cplusplus
 }
 #endif

@@ -96,6 +96,8 @@ _SIGS = {
     "sm_nonfinite": (_c_i32, [_c_p, _c_i64, _c_p, _c_p]),
     "sm_adamw": (_c_i32, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_i64, _c_f32, _c_f32, _c_f32, _c_f32, _c_f32, _c_p, _c_p,
                           _c_i32, _c_p]),
+    "sm_fedavg_weighted_sum": (_c_i32, [_c_i32, _c_p, _c_p, _c_i64, _c_p, _c_p]),
+    "sm_fedavg_counters_max": (_c_i32, [_c_i32, _c_p, _c_i64, _c_p, _c_p]),
 }
 
 _lib = None

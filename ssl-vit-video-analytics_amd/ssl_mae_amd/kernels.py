@@ -472,3 +472,41 @@ def nonfinite(g, flag):
 def adamw(p, g, m, v, lr, b1, b2, eps, wd, found_inf, step, shadow=None, advance_step=True):
     call("sm_adamw", ptr(p), ptr(g), ptr(m), ptr(v), ptr(shadow), p.numel(), float(lr), float(b1), float(b2),
          float(eps), float(wd), ptr(found_inf), ptr(step), 1 if advance_step else 0, stream())
+
+
+# ------------------------------------------------------------------ federated averaging
+def fedavg_weighted_sum(bufs, weights, out=None):
+    """out = sum_j bufs[j] * weights[j] in client order (fed_loop.py:46-49), bit-exact.
+    bufs: equal-length contiguous fp32 device tensors; weights: fp32-representable floats."""
+    import ctypes
+    if not bufs:
+        raise _lib.KernelError("fedavg_weighted_sum needs at least one client buffer")
+    _chk(*bufs)
+    n = bufs[0].numel()
+    for b in bufs:
+        if b.dtype != torch.float32 or b.numel() != n or not b.is_contiguous() or b.device != bufs[0].device:
+            raise _lib.KernelError("fedavg client buffers must be contiguous fp32 of one length on one device")
+    if out is None:
+        out = torch.empty_like(bufs[0])
+    k = len(bufs)
+    ptrs = (ctypes.c_void_p * k)(*[b.data_ptr() for b in bufs])
+    ws = (ctypes.c_float * k)(*[float(w) for w in weights])
+    call("sm_fedavg_weighted_sum", k, ctypes.cast(ptrs, ctypes.c_void_p), ctypes.cast(ws, ctypes.c_void_p), n,
+         ptr(out), stream())
+    return out
+
+
+def fedavg_counters_max(bufs, out=None):
+    """out = elementwise max over clients of int64 counters (fed_loop.py:52-55)."""
+    import ctypes
+    _chk(*bufs)
+    n = bufs[0].numel()
+    for b in bufs:
+        if b.dtype != torch.int64 or b.numel() != n or not b.is_contiguous():
+            raise _lib.KernelError("fedavg counters must be contiguous int64 of one length")
+    if out is None:
+        out = torch.empty_like(bufs[0])
+    k = len(bufs)
+    ptrs = (ctypes.c_void_p * k)(*[b.data_ptr() for b in bufs])
+    call("sm_fedavg_counters_max", k, ctypes.cast(ptrs, ctypes.c_void_p), n, ptr(out), stream())
+    return out

@@ -1,0 +1,130 @@
+"""FedAvg on the GPU through the C ABI (sm_fedavg_weighted_sum / _counters_max):
+bit-exact against the oracle and the reference's golden aggregate, ragged and
+misaligned buffers, client-count limits, and the full MAE model state."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_sum(arrs, weights):
+    from oracle import fedavg_oracle as O
+    return O.weighted_sum(arrs, weights)
+
+
+@pytest.mark.parametrize("n,k", [(1, 1), (3, 2), (4096, 4), (1_000_003, 3), (257, 32)])
+def test_weighted_sum_bit_exact(n, k):
+    from ssl_mae_amd import federated as F
+    from ssl_mae_amd import kernels as K
+    rng = np.random.default_rng(n + k)
+    arrs = [(rng.standard_normal(n) * 10 ** rng.uniform(-3, 3)).astype(np.float32) for _ in range(k)]
+    w = [float(x) for x in rng.integers(1, 1000, k)]
+    norm = F._norm_weights(w, float(sum(w)))
+    out = K.fedavg_weighted_sum([torch.from_numpy(a).cuda() for a in arrs], norm)
+    assert np.array_equal(out.cpu().numpy(), _oracle_sum(arrs, w))
+
+
+def test_weighted_sum_misaligned_scalar_path():
+    from ssl_mae_amd import federated as F
+    from ssl_mae_amd import kernels as K
+    rng = np.random.default_rng(9)
+    base = [torch.from_numpy(rng.standard_normal(1031).astype(np.float32)).cuda() for _ in range(3)]
+    views = [b[1:] for b in base]          # 4-byte offset: not 16-B aligned
+    w = [2.0, 5.0, 11.0]
+    out = K.fedavg_weighted_sum(views, F._norm_weights(w, 18.0))
+    assert np.array_equal(out.cpu().numpy(), _oracle_sum([v.cpu().numpy() for v in views], w))
+
+
+def test_client_limits_and_empty():
+    from ssl_mae_amd import kernels as K
+    from ssl_mae_amd._lib import KernelError
+    bufs = [torch.zeros(8, device="cuda") for _ in range(33)]
+    with pytest.raises(KernelError):
+        K.fedavg_weighted_sum(bufs, [1.0] * 33)
+    e = K.fedavg_weighted_sum([torch.zeros(0, device="cuda")], [1.0])
+    assert e.numel() == 0
+
+
+def test_counters_max():
+    from ssl_mae_amd import kernels as K
+    c = [torch.tensor([3, -5, 1 << 40, 7], dtype=torch.int64, device="cuda"),
+         torch.tensor([9, -6, 2, 7], dtype=torch.int64, device="cuda")]
+    assert K.fedavg_counters_max(c).tolist() == [9, -5, 1 << 40, 7]
+
+
+def test_fedavg_aggregate_matches_reference_golden():
+    """Golden from running src/federated/fed_loop.py:fedavg_aggregate."""
+    import torch.nn as nn
+    from ssl_mae_amd import federated as F
+    z = np.load(os.path.join(GOLDEN, "fedavg.npz"))
+    keys = [str(k) for k in z["keys"]]
+
+    class Net(nn.Module):   # same entries as make_golden_fedavg.Net(extra=True)
+        def __init__(self):
+            super().__init__()
+            self.conv = nn.Conv2d(3, 8, 3, bias=False)
+            self.bn = nn.BatchNorm2d(8)
+            self.fc = nn.Linear(37, 13)
+            self.register_buffer("idx", torch.arange(5, dtype=torch.int32))
+            self.register_buffer("extra", torch.zeros(3))
+
+    g = Net().cuda()
+    g.load_state_dict({k: torch.from_numpy(z[f"global/{k}"]) for k in keys})
+    clients = []
+    for i in range(3):
+        pre = f"client{i}/"
+        clients.append({k[len(pre):]: torch.from_numpy(z[k]).cuda() for k in z.files if k.startswith(pre)})
+    new = F.fedavg_aggregate(g, clients, [float(x) for x in z["weights"]])
+    assert list(new) == keys
+    for k in keys:
+        got = new[k].cpu().numpy()
+        assert got.dtype == z[f"out/{k}"].dtype, k
+        assert np.array_equal(got, z[f"out/{k}"]), k
+        assert np.array_equal(g.state_dict()[k].cpu().numpy(), z[f"out/{k}"]), k
+
+
+def test_fedavg_full_mae_state_bit_exact_and_properties():
+    """Four MAE clients (TinyViT-21M variant + 4x384 decoder, ~24 M fp32 entries)."""
+    from oracle import fedavg_oracle as O
+    from ssl_mae_amd import federated as F
+    from ssl_mae_amd.mae_vit_adapter import TinyVideoMAE
+    from ssl_mae_amd.tiny_vit import tiny_vit_21m_variant
+    cfg = {"dataset": {"clip_len": 8, "image_size": 224},
+           "model": {"decoder_embed_dim": 384, "decoder_depth": 4, "decoder_num_heads": 6}}
+    models = []
+    for s in range(5):
+        torch.manual_seed(s)
+        models.append(TinyVideoMAE(tiny_vit_21m_variant(img_size=224), cfg).cuda())
+    glob, clients = models[0], models[1:]
+    for i, c in enumerate(clients):
+        for name, b in c.named_buffers():
+            if "num_batches_tracked" in name:
+                b.fill_(3 * i + 1)
+    states = [{k: v.detach().clone() for k, v in c.state_dict().items()} for c in clients]
+    w = [1200.0, 800.0, 1500.0, 500.0]
+    new = F.fedavg_aggregate(glob, states, w)
+    np_states = [{k: v.cpu().numpy() for k, v in s.items()} for s in states]
+    expect = O.fedavg_aggregate({k: v.cpu().numpy() for k, v in glob.state_dict().items()}, np_states, w)
+    n_float = 0
+    for k, v in expect.items():
+        got = new[k].cpu().numpy()
+        assert np.array_equal(got, v), k
+        n_float += v.size if v.dtype == np.float32 else 0
+    assert n_float > 20_000_000
+    # one client with all the weight -> its floating-point state exactly (counters: max)
+    new1 = F.fedavg_aggregate(glob, states, [0.0, 5.0, 0.0, 0.0])
+    for k, v in states[1].items():
+        if v.is_floating_point():
+            assert torch.equal(new1[k], v), k
+        elif "num_batches_tracked" in k:
+            assert int(new1[k]) == 10, k
+    # world-size-1 allgather path equals a one-client aggregate (identity)
+    before = {k: v.detach().clone() for k, v in clients[2].state_dict().items()}
+    F.fedavg_allgather(clients[2], 7.0)
+    for k, v in clients[2].state_dict().items():
+        assert torch.equal(v, before[k]), k
