@@ -205,6 +205,15 @@ int sm_fedavg_weighted_sum(int num_clients, const float* const* client_bufs, con
 int sm_fedavg_counters_max(int num_clients, const int64_t* const* client_counters, int64_t n, int64_t* out,
                            hipStream_t st);
 
+/* ---- clip input pipeline (src/train_ssl_mae.py:137-141 PILToTensor + ConvertImageDtype +
+ * Normalize; src/datasets/mae_loader.py:70-77 BGR swap img[[2,1,0]] and [C,T,H,W] stack).
+ * frames uint8 [B][T][H][W][3] (decoded RGB) -> out fp32 [B][3][T][H][W],
+ * out = (u / 255 - mean[s]) / std[s] with s = 2 - c when bgr_swap (IEEE division,
+ * bit-identical to the CPU transform); valid[b] == 0 (nullable) writes a zero clip
+ * (mae_loader.py:35-43).  mean3 / std3 are HOST arrays of 3 floats. */
+int sm_frames_normalize(const uint8_t* frames, const uint8_t* valid, int B, int T, int H, int W, const float* mean3,
+                        const float* std3, int bgr_swap, float* out, hipStream_t st);
+
 #ifdef __cplusplus
 }
 #endif

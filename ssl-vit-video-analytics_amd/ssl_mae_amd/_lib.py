@@ -98,6 +98,7 @@ _SIGS = {
                           _c_i32, _c_p]),
     "sm_fedavg_weighted_sum": (_c_i32, [_c_i32, _c_p, _c_p, _c_i64, _c_p, _c_p]),
     "sm_fedavg_counters_max": (_c_i32, [_c_i32, _c_p, _c_i64, _c_p, _c_p]),
+    "sm_frames_normalize": (_c_i32, [_c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_i32, _c_p, _c_p]),
 }
 
 _lib = None

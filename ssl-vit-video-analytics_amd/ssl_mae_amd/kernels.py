@@ -510,3 +510,23 @@ def fedavg_counters_max(bufs, out=None):
     ptrs = (ctypes.c_void_p * k)(*[b.data_ptr() for b in bufs])
     call("sm_fedavg_counters_max", k, ctypes.cast(ptrs, ctypes.c_void_p), n, ptr(out), stream())
     return out
+
+
+# ------------------------------------------------------------------ clip input pipeline
+def frames_normalize(frames, mean, std, bgr_swap=True, valid=None, out=None):
+    """uint8 [B,T,H,W,3] decoded frames -> fp32 [B,3,T,H,W] normalised clip
+    (train_ssl_mae.py:137-141 transform + mae_loader.py:70-77 BGR swap / permute)."""
+    import ctypes
+    _chk(frames, valid)
+    if frames.dtype != torch.uint8 or frames.dim() != 5 or frames.shape[-1] != 3 or not frames.is_contiguous():
+        raise _lib.KernelError("frames must be contiguous uint8 [B,T,H,W,3]")
+    B, T, H, W, _ = frames.shape
+    if valid is not None and (valid.dtype not in (torch.uint8, torch.bool) or valid.numel() != B):
+        raise _lib.KernelError("valid must be uint8/bool [B]")
+    if out is None:
+        out = torch.empty((B, 3, T, H, W), dtype=torch.float32, device=frames.device)
+    m = (ctypes.c_float * 3)(*[float(x) for x in mean])
+    s = (ctypes.c_float * 3)(*[float(x) for x in std])
+    call("sm_frames_normalize", ptr(frames), ptr(valid), B, T, H, W, ctypes.cast(m, ctypes.c_void_p),
+         ctypes.cast(s, ctypes.c_void_p), 1 if bgr_swap else 0, ptr(out), stream())
+    return out
