@@ -1,0 +1,88 @@
+"""Full-MAE checkpoint and resume (SURVEY.md §5 "Checkpoint / resume", §8(f) rank 4).
+
+The reference saves only the encoder every 10 epochs
+(`src/train_ssl_mae.py:190-194` -> `utils.save_checkpoint`, `src/utils.py:73-77`):
+no decoder, no optimizer state, no resume.  The build keeps that file unchanged
+(`encoder_ep{N}.pth`, the keys `train_finetune` and FedAvg consume) and adds one
+training-state file next to it with everything needed to continue bit-for-bit:
+
+  model        full TinyVideoMAE state_dict (encoder + decoder + BN running stats)
+  optimizer    FusedAdamW state (per-name exp_avg / exp_avg_sq, step, hyper-params)
+  scaler       GradScaler shim state
+  epoch        last finished epoch
+  rng          torch CPU generator (drives the tube mask), device generator seeds,
+               numpy / python RNG (drive the loader's frame-index choice)
+
+Everything is a tensor / number / string, so `torch.load(..., weights_only=True)`
+reads it back.
+"""
+import random
+from pathlib import Path
+
+import numpy as np
+import torch
+
+
+def _rng_state():
+    np_state = np.random.get_state()
+    py = random.getstate()
+    st = {"torch_cpu": torch.get_rng_state(),
+          "numpy_keys": torch.from_numpy(np_state[1].astype(np.int64)),
+          "numpy_pos": int(np_state[2]), "numpy_has_gauss": int(np_state[3]), "numpy_gauss": float(np_state[4]),
+          "python_version": int(py[0]), "python_state": torch.tensor(py[1], dtype=torch.int64)}
+    if torch.cuda.is_available():
+        st["cuda_seeds"] = torch.tensor([g.initial_seed() for g in torch.cuda.default_generators],
+                                        dtype=torch.int64)
+    return st
+
+
+def _set_rng_state(st):
+    torch.set_rng_state(st["torch_cpu"])
+    np.random.set_state(("MT19937", st["numpy_keys"].numpy().astype(np.uint32), int(st["numpy_pos"]),
+                         int(st["numpy_has_gauss"]), float(st["numpy_gauss"])))
+    random.setstate((int(st["python_version"]), tuple(int(v) for v in st["python_state"].tolist()), None))
+    if "cuda_seeds" in st and torch.cuda.is_available():
+        for g, s in zip(torch.cuda.default_generators, st["cuda_seeds"].tolist()):
+            g.manual_seed(int(s))
+
+
+def save_training_state(path, model, optimizer, scaler, epoch):
+    """Write the full resumable state of an MAE run to `path`."""
+    path = Path(path)
+    path.parent.mkdir(parents=True, exist_ok=True)
+    state = {"model": {k: v.detach().cpu() for k, v in model.state_dict().items()},
+             "optimizer": _to_cpu(optimizer.state_dict()),
+             "scaler": scaler.state_dict() if scaler is not None else {},
+             "epoch": int(epoch),
+             "forward_count": int(getattr(model, "_sm_fwd_count", 0)),
+             "rng": _rng_state()}
+    tmp = path.with_suffix(path.suffix + ".tmp")
+    torch.save(state, tmp)
+    tmp.replace(path)
+    return path
+
+
+def load_training_state(path, model, optimizer, scaler=None):
+    """Restore a state written by save_training_state; returns the epoch to start
+    from (last finished epoch + 1)."""
+    state = torch.load(path, map_location="cpu", weights_only=True)
+    model.load_state_dict(state["model"], strict=True)
+    from .mae_vit_adapter import ensure_flat
+    from .functions import Mode
+    ensure_flat(model, Mode(False))       # parameters live in the flat buffer before the optimizer state
+    optimizer.load_state_dict(state["optimizer"])
+    if scaler is not None and state.get("scaler"):
+        scaler.load_state_dict(state["scaler"])
+    model._sm_fwd_count = int(state.get("forward_count", 0))
+    _set_rng_state(state["rng"])
+    return int(state["epoch"]) + 1
+
+
+def _to_cpu(x):
+    if torch.is_tensor(x):
+        return x.detach().cpu()
+    if isinstance(x, dict):
+        return {k: _to_cpu(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return type(x)(_to_cpu(v) for v in x)
+    return x

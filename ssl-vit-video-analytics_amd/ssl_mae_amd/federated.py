@@ -79,13 +79,21 @@ def fedavg_aggregate(global_model, client_states, client_weights):
 
     new_state = {}
     float_keys, count_keys = [], []
+    norm = _norm_weights(client_weights, total_w)
     for k, g in global_state.items():
         if any(k not in cs for cs in client_states):
             new_state[k] = g.detach().clone()
         elif _is_float_tensor(g):
-            if g.dtype != torch.float32:
-                raise RuntimeError(f"FedAvg kernel aggregates fp32 state only; {k} is {g.dtype}")
-            float_keys.append(k)
+            if g.dtype == torch.float32:
+                float_keys.append(k)
+            else:
+                # fp16 / bf16 / fp64 entries (not produced by the MAE models): the
+                # reference's per-key accumulation in the entry's own dtype
+                # (fed_loop.py:46-49), as device tensor ops on the global model's GPU.
+                acc = torch.zeros_like(g.detach())
+                for cs, w in zip(client_states, client_weights):
+                    acc += cs[k].detach().to(device=device, dtype=acc.dtype) * (float(w) / total_w)
+                new_state[k] = acc
         elif "num_batches_tracked" in k:
             count_keys.append(k)
         else:
@@ -93,7 +101,7 @@ def fedavg_aggregate(global_model, client_states, client_weights):
 
     if float_keys:
         bufs = [_flat([cs[k] for k in float_keys], device, torch.float32) for cs in client_states]
-        out = K.fedavg_weighted_sum(bufs, _norm_weights(client_weights, total_w))
+        out = K.fedavg_weighted_sum(bufs, norm)
         _unflat(out, float_keys, global_state, new_state)
     if count_keys:
         bufs = [_flat([cs[k] for k in count_keys], device, torch.int64) for cs in client_states]
@@ -128,7 +136,8 @@ def fedavg_allgather(model, weight, group=None, combine=None):
     other_keys = [k for k, v in state.items() if not _is_float_tensor(v) and "num_batches_tracked" not in k]
     for k in float_keys:
         if state[k].dtype != torch.float32:
-            raise RuntimeError(f"FedAvg aggregates fp32 state only; {k} is {state[k].dtype}")
+            raise RuntimeError(f"fedavg_allgather aggregates fp32 state only; {k} is {state[k].dtype} "
+                               "(use fedavg_aggregate, which follows the reference for any float dtype)")
 
     w = torch.tensor([float(weight)], dtype=torch.float64, device=device)
     ws = [torch.empty_like(w) for _ in range(world)]

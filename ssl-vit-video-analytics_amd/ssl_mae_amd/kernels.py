@@ -482,6 +482,8 @@ def fedavg_weighted_sum(bufs, weights, out=None):
     if not bufs:
         raise _lib.KernelError("fedavg_weighted_sum needs at least one client buffer")
     _chk(*bufs)
+    if len(weights) != len(bufs):
+        raise _lib.KernelError(f"fedavg_weighted_sum: {len(bufs)} client buffers but {len(weights)} weights")
     n = bufs[0].numel()
     for b in bufs:
         if b.dtype != torch.float32 or b.numel() != n or not b.is_contiguous() or b.device != bufs[0].device:
@@ -499,11 +501,13 @@ def fedavg_weighted_sum(bufs, weights, out=None):
 def fedavg_counters_max(bufs, out=None):
     """out = elementwise max over clients of int64 counters (fed_loop.py:52-55)."""
     import ctypes
+    if not bufs:
+        raise _lib.KernelError("fedavg_counters_max needs at least one client buffer")
     _chk(*bufs)
     n = bufs[0].numel()
     for b in bufs:
-        if b.dtype != torch.int64 or b.numel() != n or not b.is_contiguous():
-            raise _lib.KernelError("fedavg counters must be contiguous int64 of one length")
+        if b.dtype != torch.int64 or b.numel() != n or not b.is_contiguous() or b.device != bufs[0].device:
+            raise _lib.KernelError("fedavg counters must be contiguous int64 of one length on one device")
     if out is None:
         out = torch.empty_like(bufs[0])
     k = len(bufs)

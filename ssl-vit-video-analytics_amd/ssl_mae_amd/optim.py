@@ -150,9 +150,44 @@ class FusedAdamW:
         return None
 
     def state_dict(self):
+        """torch.optim-style state: per-parameter `exp_avg` / `exp_avg_sq` keyed by the
+        parameter's name in the flat buffer (layout-independent), plus the shared
+        step count.  Tensors are clones (safe to torch.save while training goes on)."""
+        groups = [{k: v for k, v in self.param_groups[0].items() if k != "params"}]
         st = self._state
-        return {"param_groups": [{k: v for k, v in self.param_groups[0].items() if k != "params"}],
-                "state": None if st is None else {"m": st["m"], "v": st["v"], "step": st["step"]}}
+        if st is None:
+            return {"param_groups": groups, "state": {}, "step": 0}
+        flat = st["flat"]
+        mine = {id(p) for p in self.param_list}
+        per = {}
+        for name, p, off in zip(flat.names, flat.params, flat.offsets):
+            if id(p) not in mine:
+                continue
+            n = p.numel()
+            per[name] = {"exp_avg": st["m"][off:off + n].view(p.shape).clone(),
+                         "exp_avg_sq": st["v"][off:off + n].view(p.shape).clone()}
+        return {"param_groups": groups, "state": per, "step": int(st["step"].item())}
+
+    def load_state_dict(self, sd):
+        """Inverse of state_dict (the model must have run its flat-buffer setup, e.g.
+        one forward or `ensure_flat`)."""
+        if self._state is None:
+            self._init_state()
+        st = self._state
+        flat = st["flat"]
+        g = sd.get("param_groups", [{}])[0]
+        for k in ("lr", "betas", "eps", "weight_decay"):
+            if k in g:
+                self.param_groups[0][k] = tuple(g[k]) if k == "betas" else g[k]
+        by_name = dict(zip(flat.names, zip(flat.params, flat.offsets)))
+        for name, s in sd.get("state", {}).items():
+            if name not in by_name:
+                raise KeyError(f"optimizer state for unknown parameter {name}")
+            p, off = by_name[name]
+            n = p.numel()
+            st["m"][off:off + n].copy_(s["exp_avg"].reshape(-1).to(st["m"].device))
+            st["v"][off:off + n].copy_(s["exp_avg_sq"].reshape(-1).to(st["v"].device))
+        st["step"].fill_(int(sd.get("step", 0)))
 
 
 class GradScaler:
@@ -174,6 +209,12 @@ class GradScaler:
 
     def get_scale(self):
         return 1.0
+
+    def state_dict(self):
+        return {"scale": 1.0, "enabled": self.enabled}
+
+    def load_state_dict(self, sd):
+        self.enabled = bool(sd.get("enabled", self.enabled))
 
     def unscale_(self, optimizer):
         pass

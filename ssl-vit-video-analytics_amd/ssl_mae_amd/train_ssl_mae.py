@@ -7,7 +7,11 @@ masked normalised-pixel MSE -> zero_grad / backward / step -> `loss.item()` ever
 step, and every `log_interval` steps the masked-prediction std and throughput
 (log_interval * batch_size / elapsed).  `main()` honours `--config` (the
 reference hard-codes the path, :130) and runs the loop the reference's :168
-TypeError prevents.
+TypeError prevents.  The loader is the MI355X clip pipeline of mae_loader
+(uint8 frames, one H2D copy, sm_frames_normalize on the GPU); a loader that yields
+ready fp32 clips (the reference's transform path) is accepted as well.  Every 10
+epochs the reference's encoder-only file is written, plus a full training-state
+file (`checkpoint.py`) that `--resume` continues from.
 """
 import argparse
 import logging
@@ -19,7 +23,8 @@ import torch
 
 from . import kernels as K
 from .functions import mae_loss, masked_pred_std
-from .mae_loader import tube_mask_with_index
+from .checkpoint import load_training_state, save_training_state
+from .mae_loader import ClipNormalizer, LazyVideoMAEDataset, collate_frames, tube_mask_with_index
 from .mae_vit_adapter import TinyVideoMAE
 from .optim import FusedAdamW, GradScaler
 from .tiny_vit import tiny_vit_21m_variant
@@ -68,8 +73,20 @@ def train_step(model, clip, optimizer, scaler, ssl_cfg, bf16=True):
     return loss, pred, idx
 
 
-def train_one_epoch(model, loader, optimizer, scaler, epoch, device, config, writer, logger):
+def _to_clip(batch, device, normalizer):
+    """A loader batch -> fp32 clip [B,3,T,H,W] on the device: (uint8 frames, valid)
+    from the transform=None dataset goes through sm_frames_normalize; a tensor is a
+    ready clip (reference transform path)."""
+    if isinstance(batch, (tuple, list)):
+        frames, valid = batch
+        return normalizer(frames, valid)
+    return batch.to(device, non_blocking=True)
+
+
+def train_one_epoch(model, loader, optimizer, scaler, epoch, device, config, writer, logger, normalizer=None):
     model.train()
+    if normalizer is None:
+        normalizer = ClipNormalizer(device=device)
     ssl_cfg = config["ssl"]
     train_cfg = config["training"]
     num_steps = len(loader)
@@ -77,8 +94,8 @@ def train_one_epoch(model, loader, optimizer, scaler, epoch, device, config, wri
     epoch_start = time.time()
     last_log = time.time()
     total_loss = 0.0
-    for step, clip in enumerate(loader):
-        clip = clip.to(device, non_blocking=True)
+    for step, batch in enumerate(loader):
+        clip = _to_clip(batch, device, normalizer)
         loss, pred, idx = train_step(model, clip, optimizer, scaler, ssl_cfg)
         total_loss += loss.item()
         if step % train_cfg["log_interval"] == 0 and step > 0:
@@ -100,9 +117,19 @@ def build_model(cfg, device="cuda"):
     return TinyVideoMAE(encoder, cfg).to(device)
 
 
+def make_loader(ds, batch_size, num_workers=16, shuffle=True):
+    """train_ssl_mae.py:154-161 (16 workers, pinned memory, prefetch 2) over the
+    uint8-frame dataset (collate_frames)."""
+    kw = {"prefetch_factor": 2} if num_workers > 0 else {}
+    return torch.utils.data.DataLoader(ds, batch_size=batch_size, shuffle=shuffle, num_workers=num_workers,
+                                       pin_memory=True, collate_fn=collate_frames, **kw)
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="configs/ssl_mae.yaml")
+    ap.add_argument("--resume", default=None, help="training-state file written by a previous run")
+    ap.add_argument("--max-steps", type=int, default=None, help="stop each epoch after this many steps")
     args = ap.parse_args(argv)
     cfg = load_config(args.config)
     set_seed(42)
@@ -114,24 +141,61 @@ def main(argv=None):
     except Exception:
         writer = NullWriter()
     model = build_model(cfg, device)
-    from .data import LazyVideoMAEDataset, make_loader
     ds = LazyVideoMAEDataset(split_file=cfg["dataset"]["train_split"], clip_len=cfg["dataset"]["clip_len"],
                              stride=cfg["dataset"]["stride"], image_size=cfg["dataset"]["image_size"])
-    loader = make_loader(ds, cfg["training"]["batch_size"], cfg["training"].get("num_workers", 8))
+    loader = make_loader(ds, cfg["training"]["batch_size"], int(cfg["training"].get("num_workers", 16)))
+    if args.max_steps is not None:
+        loader = _Limited(loader, args.max_steps)
     optimizer = FusedAdamW(model.parameters(), lr=float(cfg["training"]["lr"]),
                            weight_decay=float(cfg["training"].get("weight_decay", 0.05)))
     scaler = GradScaler("cuda")
-    logger.info(f"STARTING PRETRAINING | epochs {cfg['training']['epochs']} | image {cfg['dataset']['image_size']} | "
-                f"mask ratio {cfg['ssl']['mask_ratio']} | clip_len {cfg['dataset']['clip_len']}")
+    start = 1
+    if args.resume:
+        start = load_training_state(args.resume, model, optimizer, scaler)
+        logger.info(f"Resumed from {args.resume} at epoch {start}")
+    normalizer = ClipNormalizer(device=device)
+    logger.info("=" * 50)
+    logger.info(f"STARTING PRETRAINING | Total Epochs: {cfg['training']['epochs']}")
+    logger.info(f"image size: {cfg['dataset']['image_size']} | Mask Ratio: {cfg['ssl']['mask_ratio']} | "
+                f"clip_len: {cfg['dataset']['clip_len']}  | datasets: {cfg['dataset']['train_split']}")
+    logger.info("=" * 50)
     t0 = time.time()
-    for epoch in range(1, cfg["training"]["epochs"] + 1):
-        avg, dur = train_one_epoch(model, loader, optimizer, scaler, epoch, device, cfg, writer, logger)
-        logger.info(f"==> Epoch {epoch} | Average Loss: {avg:.4f} | Time: {format_time(dur)} | "
-                    f"Cumulative: {format_time(time.time() - t0)}")
+    save_dir = Path(cfg["training"]["save_dir"])
+    epochs = cfg["training"]["epochs"]
+    for epoch in range(start, epochs + 1):
+        avg, dur = train_one_epoch(model, loader, optimizer, scaler, epoch, device, cfg, writer, logger,
+                                   normalizer)
+        total = time.time() - t0
+        eta = total / (epoch - start + 1) * (epochs - epoch)
+        logger.info("-" * 30)
+        logger.info(f"==> Epoch {epoch} SUMMARY")
+        logger.info(f"    Average Loss: {avg:.4f}")
+        logger.info(f"    Training Time: {format_time(dur)}")
+        logger.info(f"    Cumulative Time: {format_time(total)}")
+        logger.info(f"    Total Training ETA: {format_time(eta)}")
+        logger.info("-" * 30)
         if epoch % 10 == 0:
-            p = Path(cfg["training"]["save_dir"]) / f"encoder_ep{epoch}.pth"
+            p = save_dir / f"encoder_ep{epoch}.pth"
             save_checkpoint(model.encoder.state_dict(), p)
+            save_training_state(save_dir / "last_state.pth", model, optimizer, scaler, epoch)
             logger.info(f"Checkpoint saved to {p}")
+    return model
+
+
+class _Limited:
+    """First `n` batches of a loader (smoke runs of main())."""
+
+    def __init__(self, loader, n):
+        self.loader, self.n = loader, int(n)
+
+    def __len__(self):
+        return min(len(self.loader), self.n)
+
+    def __iter__(self):
+        for i, b in enumerate(self.loader):
+            if i >= self.n:
+                break
+            yield b
 
 
 if __name__ == "__main__":

@@ -1,0 +1,364 @@
+"""BASELINE config 2 (bf16, B=256 clips, T=8, 224x224) exercised at its own shapes.
+
+The benchmarked path dispatches the bf16 kernels (MFMA flash attention with the
+counter-hash dropout, the v2 GEMM with 1-D XCD-remapped grids, the fused
+MBConv depthwise / SE / BN kernels).  These tests run those kernels at the bench's
+sequence lengths, channel counts and grid sizes and compare them with a plain
+fp32 PyTorch reference of the same op computed from the SAME bf16-rounded inputs
+(torch on the GPU, fp32 math; for dropout the reference applies the host
+regeneration of the kernel's keep mask).
+
+Tolerances (bf16 operands, fp32 accumulation, bf16 outputs):
+  * elementwise outputs / gradients: max |err| <= 2e-2 x max |ref| (3e-2 for the
+    attention backward, whose dS = P (dP - Delta) cancels);
+  * channel reductions (BN / weight gradients): 2e-2 relative to max (3e-2 for
+    BN0 of the MBConv, two bf16-stored gradients upstream);
+  * whole-model bf16 step vs the reference's fp32 golden: loss within 2 %, per
+    parameter gradient cosine > 0.98 and gradient norm within 10 %.
+Full-size (B=256) runs are checked on sampled heads / rows plus size-independent
+properties (linearity of the GEMM over rows, finiteness, BN counters).
+"""
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+B_BENCH, T_BENCH, S_BENCH = 256, 8, 224
+L_DEC = T_BENCH * (S_BENCH // 8) ** 2          # 6272 decoder tokens per clip
+FRAMES = B_BENCH * T_BENCH                     # 2048 frames per step
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from ssl_mae_amd import _lib
+    _lib.load()
+
+
+def KK():
+    from ssl_mae_amd import kernels
+    return kernels
+
+
+def rel(a, b):
+    a = a.detach().float()
+    b = b.detach().float().to(a.device)
+    return ((a - b).abs().max() / (b.abs().max() + 1e-12)).item()
+
+
+def _randn(shape, seed, dtype=torch.bfloat16, scale=1.0, shift=0.0):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    return (torch.randn(shape, generator=g, device=DEV) * scale + shift).to(dtype)
+
+
+# ------------------------------------------------------------------ attention
+def _attn_keep(n, h, H, L, p, seed, device=DEV):
+    """Keep mask [L, L] of head (n, h): torch restatement of the attention kernels'
+    counter hash (csrc/attention.hip, mix24 + 7-bit threshold), as in
+    test_kernels_gpu._np_keep(attn=True)."""
+    M = 0xFFFFFFFF
+    s32 = (seed & M) ^ (seed >> 32)
+    r = ((n * H + h) * L + torch.arange(L, device=device, dtype=torch.int64))[:, None]
+    c = torch.arange(L, device=device, dtype=torch.int64)[None, :]
+    x = (s32 + r * 0x9E3779B1 + (c >> 2) * 0x7FEB352D) & M
+    x = x ^ (x >> 16)
+    x = ((x & 0xFFFFFF) * 0xEBCA6B) & M
+    x = x ^ (x >> 13)
+    x = ((x & 0xFFFFFF) * 0xB2AE35) & M
+    x = x ^ (x >> 16)
+    byte = (x >> ((c & 3) * 8)) & 0xFF
+    return (byte & 0x7F) >= int(p * 128 + 0.5)
+
+
+def _head_ref(qkv, dO, n, h, N, L, H, D, p, seed):
+    """fp32 forward + gradients of one (sample, head) of packed qkv [N*L, 3*H*D]."""
+    t = qkv.view(N, L, 3, H, D)[n, :, :, h, :].float()            # [L, 3, D]
+    q, k, v = [t[:, i, :].clone().requires_grad_(True) for i in range(3)]
+    P = torch.softmax((q @ k.t()) / math.sqrt(D), -1)
+    if p > 0:
+        P = P * _attn_keep(n, h, H, L, p, seed) / (1 - p)
+    o = P @ v
+    do = dO.view(N, L, H, D)[n, :, h, :].float()
+    o.backward(do)
+    return o.detach(), q.grad, k.grad, v.grad
+
+
+def _check_heads(qkv, dO, o, dqkv, N, L, H, D, p, seed, heads):
+    for n, h in heads:
+        o_r, dq_r, dk_r, dv_r = _head_ref(qkv, dO, n, h, N, L, H, D, p, seed)
+        assert rel(o.view(N, L, H, D)[n, :, h, :], o_r) < 2e-2, ("O", n, h)
+        g = dqkv.view(N, L, 3, H, D)[n, :, :, h, :]
+        for i, ref in enumerate((dq_r, dk_r, dv_r)):
+            assert rel(g[:, i, :], ref) < 3e-2, ("dqkv", i, n, h)
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_decoder_attention_d64_full_L(p):
+    """Decoder self-attention at the bench's L = 6272 (T=8, 224^2), 6 heads, d=64,
+    with and without the probability dropout of nn.TransformerEncoderLayer."""
+    N, L, H, D, seed = 2, L_DEC, 6, 64, 0x1234_5678_9ABC
+    qkv = _randn((N * L, 3 * H * D), 1)
+    dO = _randn((N * L, H * D), 2)
+    kk = KK()
+    o, lse = kk.attn_fwd(qkv, N, L, H, D, p, seed)
+    dqkv = kk.attn_bwd(qkv, o, dO, lse, N, L, H, D, p, seed)
+    torch.cuda.synchronize()
+    _check_heads(qkv, dO, o, dqkv, N, L, H, D, p, seed, [(0, 0), (1, 5), (1, 2)])
+
+
+@pytest.mark.parametrize("N,L,H", [(4, 3136, 6), (8, 784, 12)])
+def test_encoder_attention_d32_full_L(N, L, H):
+    """Encoder global attention of stage 1 (56^2 = 3136 tokens, 6 heads) and stage 2
+    (28^2 = 784 tokens, 12 heads), d = 32, no dropout."""
+    D = 32
+    qkv = _randn((N * L, 3 * H * D), 3 + L)
+    dO = _randn((N * L, H * D), 4 + L)
+    kk = KK()
+    o, lse = kk.attn_fwd(qkv, N, L, H, D)
+    dqkv = kk.attn_bwd(qkv, o, dO, lse, N, L, H, D)
+    torch.cuda.synchronize()
+    _check_heads(qkv, dO, o, dqkv, N, L, H, D, 0.0, 0, [(0, 0), (N - 1, H - 1), (N // 2, H // 2)])
+
+
+def test_decoder_attention_full_bench_batch_sampled_heads():
+    """The full C2 launch: N = 256 clips x 6 heads x 6272 tokens (1-D XCD-remapped
+    grid of 256*6*6272/128 blocks) with dropout 0.1; sampled heads against the fp32
+    reference, every output finite."""
+    N, L, H, D, p, seed = B_BENCH, L_DEC, 6, 64, 0.1, 987654321987
+    qkv = _randn((N * L, 3 * H * D), 5)
+    dO = _randn((N * L, H * D), 6)
+    kk = KK()
+    o, lse = kk.attn_fwd(qkv, N, L, H, D, p, seed)
+    dqkv = kk.attn_bwd(qkv, o, dO, lse, N, L, H, D, p, seed)
+    torch.cuda.synchronize()
+    assert torch.isfinite(o).all() and torch.isfinite(dqkv).all() and torch.isfinite(lse).all()
+    _check_heads(qkv, dO, o, dqkv, N, L, H, D, p, seed, [(0, 0), (97, 3), (255, 5)])
+
+
+# ------------------------------------------------------------------ GEMM at the bench's row counts
+def _gemm_rows_check(y, x, w, rows, bias=None):
+    ref = x[rows].float() @ w.float().t()
+    if bias is not None:
+        ref = ref + bias.float()
+    assert rel(y[rows], ref) < 2e-2
+
+
+@pytest.mark.parametrize("name,M,K,N", [
+    ("stage0 MBConv expand 96->384 @112^2", FRAMES * 112 * 112, 96, 384),
+    ("stage0 MBConv project 384->96 @112^2", FRAMES * 112 * 112, 384, 96),
+    ("decoder qkv 384->1152", B_BENCH * L_DEC, 384, 1152),
+])
+def test_gemm_bench_shapes(name, M, K, N):
+    """linear / linear_dx / linear_dw(_bias) at the step's real M (up to 25.7 M token
+    rows): sampled rows (first / last tiles included) against fp32, and the
+    size-independent linearity identities sum_r y[r] = (sum_r x[r]) W^T and
+    sum_r dx[r] = (sum_r dy[r]) W on the whole output."""
+    kk = KK()
+    x = _randn((M, K), 10, shift=0.3)
+    w = _randn((N, K), 11, scale=1.0 / math.sqrt(K))
+    b = _randn((N,), 12, dtype=torch.float32, scale=0.1)
+    rows = torch.cat([torch.arange(0, 256), torch.randint(0, M, (4096,), generator=torch.Generator().manual_seed(1)),
+                      torch.arange(M - 256, M)]).to(DEV)
+    y = kk.linear(x, w, b)
+    _gemm_rows_check(y, x, w, rows, b)
+    sx = torch.sum(x, 0, dtype=torch.float32).double()
+    col_ref = sx @ w.double().t() + M * b.double()
+    col = torch.sum(y, 0, dtype=torch.float32).double()
+    assert ((col - col_ref).abs().max() / col_ref.abs().max()).item() < 1e-2
+    del y
+    dy = _randn((M, N), 13, scale=0.1, shift=0.05)
+    dx = kk.linear_dx(dy, w)
+    assert rel(dx[rows], dy[rows].float() @ w.float()) < 2e-2
+    sdx = torch.sum(dx, 0, dtype=torch.float32).double()
+    sdx_ref = torch.sum(dy, 0, dtype=torch.float32).double() @ w.double()
+    assert ((sdx - sdx_ref).abs().max() / sdx_ref.abs().max()).item() < 1e-2
+    del dx
+    gw = torch.zeros(N, K, device=DEV)
+    gb = torch.zeros(N, device=DEV)
+    kk.linear_dw_bias(dy, x, gw, gb)
+    ref_w = torch.zeros(N, K, dtype=torch.float64, device=DEV)
+    for s in range(0, M, 1 << 22):                # fp32 chunks, fp64 accumulation
+        ref_w += (dy[s:s + (1 << 22)].float().t() @ x[s:s + (1 << 22)].float()).double()
+    assert rel(gw, ref_w) < 2e-2
+    assert rel(gb, torch.sum(dy, 0, dtype=torch.float32)) < 1e-3
+
+
+# ------------------------------------------------------------------ fused MBConv middle at 112^2 x 384
+class _BN:
+    def __init__(self, C):
+        self.running_mean = torch.zeros(C, device=DEV)
+        self.running_var = torch.ones(C, device=DEV)
+        self.num_batches_tracked = torch.zeros((), dtype=torch.int64, device=DEV)
+        self.momentum, self.eps = 0.1, 1e-5
+
+
+@pytest.mark.parametrize("Fr,H,C,stride", [(16, 112, 384, 1), (16, 112, 384, 2), (16, 56, 768, 2)])
+def test_mbconv_fused_middle_vs_fp32_torch(Fr, H, C, stride):
+    """BN0+GELU folded into the depthwise conv, BN2 statistics from its epilogue,
+    BN2+GELU folded into SE (sm_dwconv_fused_fwd / sm_se_fwd), and the fused
+    backward (sm_se_bn_bwd / sm_dwconv_fused_bwd / sm_bn_bwd) at the stage-0 /
+    stage-1 / stage-2 shapes, against F.batch_norm / F.gelu / F.conv2d(groups=C) /
+    SE in fp32 autograd from the same bf16 inputs."""
+    kk = KK()
+    W = H
+    R = C // 4
+    a1 = _randn((Fr * H * W, C), 20, scale=1.5, shift=0.2)
+    g0 = _randn((C,), 21, torch.float32, 0.2, 1.0)
+    b0 = _randn((C,), 22, torch.float32, 0.2)
+    wdw = _randn((C, 9), 23, torch.float32, 0.3)
+    g2 = _randn((C,), 24, torch.float32, 0.2, 1.0)
+    b2 = _randn((C,), 25, torch.float32, 0.2)
+    w1 = _randn((R, C), 26, torch.float32, 1.0 / math.sqrt(C))
+    w2 = _randn((C, R), 27, torch.float32, 1.0 / math.sqrt(R))
+    Ho = (H - 1) // stride + 1
+    dh3 = _randn((Fr * Ho * Ho, C), 28, scale=1e-3)
+
+    # fp32 torch reference (NCHW)
+    leaves = [t.clone().requires_grad_(True) for t in (a1.float(), g0, b0, wdw, g2, b2, w1, w2)]
+    xa, tg0, tb0, tw, tg2, tb2, tw1, tw2 = leaves
+    x4 = xa.view(Fr, H, W, C).permute(0, 3, 1, 2)
+    h1 = F.gelu(F.batch_norm(x4, None, None, tg0, tb0, True, 0.1, 1e-5))
+    a2r = F.conv2d(h1, tw.view(C, 1, 3, 3), None, stride, 1, 1, C)
+    h2 = F.gelu(F.batch_norm(a2r, None, None, tg2, tb2, True, 0.1, 1e-5))
+    pooled = h2.mean((2, 3))
+    gate = torch.sigmoid(torch.relu(pooled @ tw1.t()) @ tw2.t())
+    h3r = h2 * gate[:, :, None, None]
+    h3r.backward(dh3.float().view(Fr, Ho, Ho, C).permute(0, 3, 1, 2))
+
+    # HIP path, as MBConvFn runs it
+    m0, r0 = kk.bn_stats(a1)
+    act0 = (m0, r0, g0, b0, True)
+    bn2 = _BN(C)
+    a2, m2, r2 = kk.dwconv_fused(a1, act0, wdw, Fr, H, W, C, stride, bn_out=bn2)
+    assert rel(a2, a2r.permute(0, 2, 3, 1).reshape(-1, C)) < 2e-2
+    assert int(bn2.num_batches_tracked) == 1
+    a2f = a2r.detach()
+    var_u = a2f.var((0, 2, 3), unbiased=True)
+    assert rel(bn2.running_var, 0.9 + 0.1 * var_u) < 2e-2
+    act2 = (m2, r2, g2, b2, True)
+    h3, pooled_k, h1se, gate_k = kk.se_fwd(a2, Fr, Ho * Ho, C, w1, w2, act=act2)
+    assert rel(gate_k, gate) < 2e-2
+    assert rel(h3, h3r.detach().permute(0, 2, 3, 1).reshape(-1, C)) < 2e-2
+    dg2 = torch.zeros(C, device=DEV)
+    db2 = torch.zeros(C, device=DEV)
+    da2, dz2, dz1 = kk.se_bn_bwd(dh3, a2, Fr, Ho * Ho, C, w1, w2, gate_k, h1se, act2, dg2, db2)
+    dw2 = torch.zeros(C, R, device=DEV)
+    dw1 = torch.zeros(R, C, device=DEV)
+    kk.gemm(dz2, h1se, dw2, C, R, Fr, 1, 1, C, R, R, beta=1.0)
+    kk.gemm(dz1, pooled_k, dw1, R, C, Fr, 1, 1, R, C, C, beta=1.0)
+    dwdw = torch.zeros(C, 9, device=DEV)
+    dh1 = kk.dwconv_fused_bwd(da2, a1, act0, wdw, dwdw, Fr, H, W, C, stride)
+    dg0 = torch.zeros(C, device=DEV)
+    db0 = torch.zeros(C, device=DEV)
+    da1 = kk.bn_bwd(dh1, a1, m0, r0, g0, b0, True, dg0, db0)
+    torch.cuda.synchronize()
+    assert rel(da1, xa.grad) < 3e-2
+    for got, ref, nm in ((dwdw, tw.grad, "w_dw"), (dg2, tg2.grad, "bn2.w"), (db2, tb2.grad, "bn2.b"),
+                         (dw1, tw1.grad, "se.fc0"), (dw2, tw2.grad, "se.fc2")):
+        assert rel(got, ref) < 2e-2, nm
+    # BN0's reductions sit behind two bf16-stored gradients (da2, dh1), as in the
+    # reference's autocast backward: 3e-2, like da1
+    for got, ref, nm in ((dg0, tg0.grad, "bn0.w"), (db0, tb0.grad, "bn0.b")):
+        assert rel(got, ref) < 3e-2, nm
+
+
+# ------------------------------------------------------------------ whole model, bf16
+def _cfg(B, T, S, ratio):
+    return {"dataset": {"clip_len": T, "image_size": S, "stride": 4, "train_split": "-"},
+            "model": {"decoder_embed_dim": 384, "decoder_depth": 4, "decoder_num_heads": 6},
+            "ssl": {"mask_ratio": ratio, "norm_pix_loss": True},
+            "training": {"batch_size": B, "lr": 5e-4, "log_interval": 20}}
+
+
+def _model(cfg, parity=True):
+    from ssl_mae_amd import parity_mode
+    from ssl_mae_amd.init_rule import apply_rule
+    from ssl_mae_amd.mae_vit_adapter import TinyVideoMAE
+    from ssl_mae_amd.tiny_vit import tiny_vit_21m_variant
+    m = TinyVideoMAE(tiny_vit_21m_variant(img_size=cfg["dataset"]["image_size"]), cfg)
+    apply_rule(m)
+    if parity:
+        parity_mode(m)
+    return m.to(DEV).train()
+
+
+def test_bf16_step_t8_224_vs_reference_golden(golden_dir):
+    """One bf16 training step at T=8, 224^2 (the C2 clip shape, B=1) against the
+    reference's fp32 step (golden) and the oracle's full fp32 gradients."""
+    from ssl_mae_amd.init_rule import synthetic_clip
+    from ssl_mae_amd.optim import FusedAdamW, GradScaler
+    from ssl_mae_amd.train_ssl_mae import train_step
+    d = np.load(os.path.join(golden_dir, "step_b1_t8_s224.npz"))
+    B, T, S, r = int(d["B"]), int(d["T"]), int(d["S"]), float(d["ratio"])
+    cfg = _cfg(B, T, S, r)
+    model = _model(cfg)
+    opt = FusedAdamW(model.parameters(), lr=5e-4, weight_decay=0.05)
+    clip = torch.from_numpy(synthetic_clip(B, T, S, seed=int(d["clip_seed"]))).to(DEV)
+    torch.manual_seed(42)
+    loss, pred, _ = train_step(model, clip, opt, GradScaler(), cfg["ssl"], bf16=True)
+    torch.cuda.synchronize()
+    gl = float(d["avg_loss"])
+    assert abs(loss.item() - gl) < 0.02 * abs(gl), (loss.item(), gl)
+    ps = pred.detach().double()
+    assert abs((ps * ps).sum().item() / float(d["pred_sumsq"]) - 1) < 0.03
+    from oracle import mae_oracle as O
+    from ssl_mae_amd.init_rule import param_value
+    P = O.make_params(cfg, param_value)
+    _, grads = O.train_step(P, None, None, clip.cpu(), torch.from_numpy(d["mask"][0]), cfg)
+    named = dict(model.named_parameters())
+    n = 0
+    for name, g in grads.items():
+        if g is None:
+            continue
+        ours = named[name]._sm_grad.detach().double().cpu().reshape(-1)
+        ref = g.double().reshape(-1)
+        gs = math.sqrt(float(d["grad_sumsq/" + name]))
+        if gs < 1e-6:        # analytically zero (a bias feeding a BatchNorm): rounding noise only
+            continue
+        assert abs(ref.norm().item() / gs - 1) < 2e-3, name       # oracle == reference (fp32)
+        cos = float(torch.dot(ours, ref) / (ours.norm() * ref.norm() + 1e-30))
+        assert cos > 0.98, (name, cos)
+        assert abs(ours.norm().item() / ref.norm().item() - 1) < 0.10, name
+        n += 1
+    assert n > 150
+
+
+def test_bf16_full_c2_step_properties():
+    """The full C2 step (B=256, T=8, 224^2, bf16, dropout/DropPath on, auto resident
+    stages) twice: finite loss near the B=1 reference value (the clips are i.i.d.),
+    finite gradients, every BN counter advanced as the reference's checkpointed
+    forward + recompute advances it, parameters updated."""
+    from ssl_mae_amd.init_rule import IMAGENET_MEAN, IMAGENET_STD
+    from ssl_mae_amd.optim import FusedAdamW, GradScaler
+    from ssl_mae_amd.train_ssl_mae import train_step
+    torch.cuda.empty_cache()
+    cfg = _cfg(B_BENCH, T_BENCH, S_BENCH, 0.75)
+    model = _model(cfg, parity=False)
+    opt = FusedAdamW(model.parameters(), lr=5e-4, weight_decay=0.05)
+    g = torch.Generator(device=DEV).manual_seed(1234)
+    mean = torch.tensor(IMAGENET_MEAN, device=DEV).view(1, 3, 1, 1, 1)
+    std = torch.tensor(IMAGENET_STD, device=DEV).view(1, 3, 1, 1, 1)
+    clip = (torch.rand(B_BENCH, 3, T_BENCH, S_BENCH, S_BENCH, generator=g, device=DEV) - mean) / std
+    torch.manual_seed(42)
+    p0 = model.decoder_pred.weight.detach().clone()
+    losses = []
+    for _ in range(2):
+        loss, pred, idx = train_step(model, clip, opt, GradScaler(), cfg["ssl"], bf16=True)
+        losses.append(loss.item())
+        flat = model._sm_flat
+        assert torch.isfinite(flat.grad[:flat.used_end]).all()
+    assert all(math.isfinite(v) for v in losses)
+    assert abs(losses[0] - 1.979) < 0.15 * 1.979, losses          # golden B=1 loss 1.979
+    assert idx.numel() == B_BENCH * T_BENCH * 588
+    assert not torch.equal(p0, model.decoder_pred.weight)
+    for name, b in model.named_buffers():
+        if name.endswith("num_batches_tracked") and ".stages.3." not in name:
+            want = 2 if "patch_embed" in name else 4      # stem once per step, stages 0-2 twice
+            assert int(b) == want, name

@@ -128,3 +128,115 @@ def test_fedavg_full_mae_state_bit_exact_and_properties():
     F.fedavg_allgather(clients[2], 7.0)
     for k, v in clients[2].state_dict().items():
         assert torch.equal(v, before[k]), k
+
+
+def test_weighted_sum_rejects_weight_count_mismatch():
+    from ssl_mae_amd import kernels as K
+    from ssl_mae_amd._lib import KernelError
+    bufs = [torch.ones(16, device="cuda") for _ in range(3)]
+    with pytest.raises(KernelError):
+        K.fedavg_weighted_sum(bufs, [0.5, 0.5])
+    with pytest.raises(KernelError):
+        K.fedavg_counters_max([torch.zeros(4, dtype=torch.int64, device="cuda"),
+                               torch.zeros(4, dtype=torch.int64)])
+
+
+def test_fedavg_aggregate_non_fp32_entries_follow_reference():
+    """fp64 / bf16 float entries are averaged in their own dtype, as fed_loop.py:46-49
+    does (fp64: bit-exact against the numpy restatement)."""
+    import torch.nn as nn
+    from ssl_mae_amd import federated as F
+
+    class Net(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.fc = nn.Linear(11, 5)
+            self.register_buffer("d64", torch.zeros(7, dtype=torch.float64))
+            self.register_buffer("h16", torch.zeros(9, dtype=torch.bfloat16))
+
+    g = Net().cuda()
+    rng = np.random.default_rng(5)
+    states = []
+    for i in range(3):
+        st = {k: v.detach().clone() for k, v in g.state_dict().items()}
+        st["fc.weight"] = torch.from_numpy(rng.standard_normal((5, 11)).astype(np.float32)).cuda()
+        st["d64"] = torch.from_numpy(rng.standard_normal(7)).cuda()
+        st["h16"] = torch.from_numpy(rng.standard_normal(9).astype(np.float32)).to(torch.bfloat16).cuda()
+        states.append(st)
+    w = [3.0, 1.0, 6.0]
+    new = F.fedavg_aggregate(g, states, w)
+    acc = np.zeros(7)
+    for st, wi in zip(states, w):
+        acc = acc + st["d64"].cpu().numpy() * (wi / 10.0)
+    assert new["d64"].dtype == torch.float64 and np.array_equal(new["d64"].cpu().numpy(), acc)
+    ref16 = sum(st["h16"].float().cpu() * (wi / 10.0) for st, wi in zip(states, w))
+    assert new["h16"].dtype == torch.bfloat16
+    assert torch.allclose(new["h16"].float().cpu(), ref16, rtol=2e-2, atol=2e-2)
+    assert np.array_equal(new["fc.weight"].cpu().numpy(),
+                          _oracle_sum([st["fc.weight"].cpu().numpy() for st in states], w))
+
+
+def _gloo_cuda_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "ssl-vit-video-analytics_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0")
+    import torch.distributed as dist
+    from ssl_mae_amd import federated as F
+    from ssl_mae_amd.mae_vit_adapter import TinyVideoMAE
+    from ssl_mae_amd.tiny_vit import tiny_vit_21m_variant
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    cfg = {"dataset": {"clip_len": 4, "image_size": 64},
+           "model": {"decoder_embed_dim": 384, "decoder_depth": 2, "decoder_num_heads": 6}}
+    torch.manual_seed(200 + rank)
+    net = TinyVideoMAE(tiny_vit_21m_variant(img_size=64), cfg).cuda()
+    with torch.no_grad():
+        for name, b in net.named_buffers():
+            if "num_batches_tracked" in name:
+                b.fill_(4 + 7 * rank)
+    before = {k: v.detach().cpu().numpy().copy() for k, v in net.state_dict().items()}
+    tot = F.fedavg_allgather(net, [300.0, 700.0][rank])       # default HIP combine
+    torch.cuda.synchronize()
+    after = {k: v.detach().cpu().numpy().copy() for k, v in net.state_dict().items()}
+    q.put((rank, tot, before, after))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_fedavg_allgather_world2_default_hip_combine():
+    """Two ranks sharing the GPU over gloo (CUDA tensors): the production
+    fedavg_allgather (fp32 all-gather + HIP weighted sum, MAX of counters, rank-0
+    broadcast of other ints) equals fedavg_aggregate of the two states, bit for bit."""
+    import socket
+    import torch.multiprocessing as mp
+    from ssl_mae_amd import federated as F
+    from ssl_mae_amd.mae_vit_adapter import TinyVideoMAE
+    from ssl_mae_amd.tiny_vit import tiny_vit_21m_variant
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gloo_cuda_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r, tot, before, after = q.get(timeout=240)
+        res[r] = (tot, before, after)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    cfg = {"dataset": {"clip_len": 4, "image_size": 64},
+           "model": {"decoder_embed_dim": 384, "decoder_depth": 2, "decoder_num_heads": 6}}
+    g = TinyVideoMAE(tiny_vit_21m_variant(img_size=64), cfg).cuda()
+    states = [{k: torch.from_numpy(v).cuda() for k, v in res[r][1].items()} for r in range(2)]
+    expect = F.fedavg_aggregate(g, states, [300.0, 700.0])
+    for r in range(2):
+        assert res[r][0] == 1000.0
+        for k, v in expect.items():
+            assert np.array_equal(res[r][2][k], v.cpu().numpy()), (r, k)
