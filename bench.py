@@ -160,7 +160,7 @@ def main():
            "model": {"decoder_embed_dim": 384, "decoder_depth": 4, "decoder_num_heads": 6},
            "ssl": {"mask_ratio": r, "norm_pix_loss": True},
            "training": {"batch_size": B, "lr": 5e-4, "log_interval": 20}}
-    torch.manual_seed(1234)                      # identical initial weights on every replica
+    torch.manual_seed(1234)
     model = build_model(cfg, dev).train()
     if args.resident:
         model.encoder.resident_stages = () if args.resident == "none" else \
@@ -186,8 +186,9 @@ def main():
         flop_per_launch = None
 
     ssl_cfg = cfg["ssl"]
-    if world > 1:
-        opt.grad_hooks.append(smdist.GradAllReduce(world))
+    # rank-0 weights/buffers broadcast; bucketed RCCL all-reduce launched from the
+    # backward on a side stream (N > 1)
+    smdist.setup_data_parallel(model, opt, world)
 
     def step(i):
         loss, _, _ = train_step(model, clips[i % 2], opt, scaler, ssl_cfg, bf16=True)

@@ -64,6 +64,12 @@ def _touch(*params):
     flat.touch(*params)
 
 
+def _done(*params):
+    """End of a backward kernel group: its gradient writes are enqueued, so the
+    data-parallel bucket(s) holding these parameters may start reducing."""
+    params[0]._sm_flat.done(*params)
+
+
 def _bn_forward(a2d, bn, gelu, residual=None, updates=1):
     mean, rstd = K.bn_stats(a2d, bn.running_mean, bn.running_var, bn.momentum, bn.eps, updates,
                             bn.num_batches_tracked)
@@ -125,6 +131,7 @@ class StemFn(torch.autograd.Function):
         dw1p = torch.empty((48, 32), dtype=torch.float32, device=a1.device)
         K.linear_dw(da1, col1, dw1p, accumulate=False)
         K.conv_wunpack_add(dw1p, G(w1), 0)
+        _done(*ctx.params)
         return (None,) * 8
 
 
@@ -229,6 +236,7 @@ class MBConvFn(torch.autograd.Function):
         x2d = x.reshape(-1, Cin)
         K.linear_dw(da1, x2d, G(w_exp).view(mid, Cin))
         dx = K.linear_dx(da1, W(w_exp, mode).view(mid, Cin), residual=dout2d if st.res else None)
+        _done(*ctx.params)
         return (dx.view(Fr, H, Wd, Cin),) + (None,) * 12
 
 
@@ -306,6 +314,7 @@ class BlockFn(torch.autograd.Function):
         dln1 = K.linear_dx(dqkv, W(wqkv, mode))
         del dqkv
         dx = K.layernorm_bwd(dln1, x, mu1, rs1, ln1w.detach(), G(ln1w), G(ln1b), dres=dx2)
+        _done(*ctx.params)
         return (dx,) + (None,) * 13
 
 
@@ -339,6 +348,7 @@ class EncToDecFn(torch.autograd.Function):
                              G(tok).reshape(D), B, T, L, D)
         K.linear_dw_bias(dy, lat, G(w), G(b))
         dlat = K.linear_dx(dy, W(w, mode))
+        _done(*ctx.params)
         return dlat, None, None, None, None, None, None, None
 
 
@@ -368,6 +378,7 @@ class HeadFn(torch.autograd.Function):
         del ln
         dln = K.linear_dx(dpred, W(w, mode))
         dx = K.layernorm_bwd(dln, x, mu, rs, lnw.detach(), G(lnw), G(lnb))
+        _done(*ctx.params)
         return dx, None, None, None, None, None
 
 

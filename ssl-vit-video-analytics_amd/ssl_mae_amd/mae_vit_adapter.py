@@ -34,6 +34,18 @@ def next_seed_base(root):
     return splitmix64((base << 20) ^ cnt)
 
 
+def make_flat(root: nn.Module, dev):
+    """Lay every parameter of `root` into one flat buffer on `dev` (see optim.FlatParams)."""
+    named = [(n, p) for n, p in root.named_parameters()]
+    mae = getattr(root, "_mae", False)
+    is_used = [not (mae and ".stages.3." in "." + n) for n, _ in named]
+    used = [np for np, u in zip(named, is_used) if u]
+    unused = [np for np, u in zip(named, is_used) if not u]
+    flat = FlatParams(gradient_order(used) + unused, dev, n_attach=len(used))
+    root._sm_flat = flat
+    return flat
+
+
 def ensure_flat(root: nn.Module, mode: Mode):
     """Move every parameter of `root` into one flat device buffer (once), then
     mark the start of a forward (zero-on-first-backward, bf16 shadow refresh)."""
@@ -43,16 +55,21 @@ def ensure_flat(root: nn.Module, mode: Mode):
         raise RuntimeError("ssl_mae_amd models run on the GPU only (move the model with .to('cuda'))")
     if flat is None or flat.device != dev or any(getattr(p, "_sm_flat", None) is not flat
                                                  for p in root.parameters()):
-        named = [(n, p) for n, p in root.named_parameters()]
-        mae = getattr(root, "_mae", False)
-        is_used = [not (mae and ".stages.3." in "." + n) for n, _ in named]
-        used = [np for np, u in zip(named, is_used) if u]
-        unused = [np for np, u in zip(named, is_used) if not u]
-        order = list(reversed(used)) + unused   # backward produces grads in reverse forward order
-        flat = FlatParams(order, dev, n_attach=len(used))
-        root._sm_flat = flat
+        flat = make_flat(root, dev)
     flat.begin_forward(mode.bf16)
     return flat
+
+
+def gradient_order(named_used):
+    """The order the backward produces gradients in: reverse forward order, except
+    that the MAE's own parameters (mask_token, temporal/spatial pos-embed) get their
+    gradients from EncToDecFn together with enc_to_dec, not after the encoder.  The
+    flat buffer follows it, so data-parallel buckets fill front to back."""
+    order = list(reversed(named_used))
+    own = [np for np in order if "." not in np[0]]
+    rest = [np for np in order if "." in np[0]]
+    at = max((i + 1 for i, (n, _) in enumerate(rest) if n.startswith("enc_to_dec.")), default=len(rest))
+    return rest[:at] + own + rest[at:]
 
 
 class _St:

@@ -52,6 +52,55 @@ class FlatParams:
         self.touched = set()
         self.fresh = False
         self.shadow_dtype_ready = False
+        # gradient buckets (data parallel): contiguous runs of whole parameters over
+        # [0, used_end); `done()` counts finished parameters per bucket and calls the
+        # ready hooks with a bucket's index as soon as its last parameter is written
+        self.bucket_ranges = []
+        self.bucket_of = {}
+        self.ready_hooks = []
+        self._pending = []
+        self._finished = set()
+
+    # ---------------------------------------------------------------- buckets
+    def make_buckets(self, bucket_elems):
+        ranges, of = [], {}
+        start = None
+        for i in range(self.n_attach):
+            s = self.offsets[i]
+            e = s + (self.params[i].numel() + ALIGN - 1) // ALIGN * ALIGN
+            if start is None:
+                start = s
+            of[id(self.params[i])] = len(ranges)
+            if e - start >= bucket_elems or i == self.n_attach - 1:
+                ranges.append((start, e))
+                start = None
+        self.bucket_ranges = ranges
+        self.bucket_of = of
+        self._reset_buckets()
+        return ranges
+
+    def _reset_buckets(self):
+        counts = [0] * len(self.bucket_ranges)
+        for b in self.bucket_of.values():
+            counts[b] += 1
+        self._pending = counts
+        self._finished = set()
+
+    def done(self, *params):
+        """Called by every backward kernel group after it has launched the writes of
+        its parameters' gradients (stream-ordered: the writes precede anything the
+        hooks enqueue on the same stream)."""
+        if not self.ready_hooks:
+            return
+        for p in params:
+            b = self.bucket_of.get(id(p))
+            if b is None or id(p) in self._finished:
+                continue
+            self._finished.add(id(p))
+            self._pending[b] -= 1
+            if self._pending[b] == 0:
+                for h in self.ready_hooks:
+                    h(b)
 
     # ---------------------------------------------------------------- per step
     def begin_forward(self, bf16):
@@ -66,6 +115,7 @@ class FlatParams:
             self.fresh = False
             K.fill_(self.grad, 0.0)
             self.touched.clear()
+            self._reset_buckets()
             for p in self.params[:self.n_attach]:
                 p.grad = p._sm_grad
         for p in params:
