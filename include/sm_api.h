@@ -71,6 +71,12 @@ int64_t sm_bn_workspace_bytes(int64_t M, int C);
 int sm_bn_stats(int x_dtype, int64_t M, int C, const void* x, float* mean, float* rstd,
                 float* run_mean, float* run_var, int64_t* num_batches_tracked, float momentum, float eps,
                 int updates, void* ws, int64_t ws_bytes, hipStream_t st);
+/* eval mode (running statistics; tiny_vit.py:16 BatchNorm2d under model.eval(),
+ * train_finetune.py:127-138 evaluate): mean = run_mean, rstd = 1/sqrt(run_var + eps),
+ * the form every BN consumer takes.  sm_bn_stats / sm_bn_bwd process C > 1024
+ * (stage-4 MBConv, 1536 channels) in column slices. */
+int sm_bn_eval_params(const float* run_mean, const float* run_var, int C, float eps, float* mean, float* rstd,
+                      hipStream_t st);
 /* statistics from per-block partials [nrows][2][C] written by a fused producer */
 int64_t sm_bn_partials_workspace_bytes(int C);
 int sm_bn_stats_from_partials(const float* part, int64_t nrows, int C, int64_t M, float* mean, float* rstd,
@@ -182,6 +188,14 @@ int sm_gather_rows(int dtype, const void* src, const int32_t* idx, int64_t nrows
                    hipStream_t st);
 int64_t sm_std_workspace_bytes(void);
 int sm_std(int dtype, const void* x, int64_t n, float* out, void* ws, int64_t ws_bytes, hipStream_t st);
+
+/* ---- fine-tune head (BASELINE config 4; src/train_finetune.py:19-40 VideoClassifier):
+ * out[g][c] = mean_r x[g][r][c] for x [G][R][C] -- per-frame embedding pooling of the
+ * channels-last encoder tokens (F.adaptive_avg_pool2d(feat, 1), mobilevit.py:164-165)
+ * and the temporal mean of the fp32 embeddings (feats.mean(dim=1), :38); backward
+ * dx[g][r][c] = dy[g][c] / R. */
+int sm_segment_mean(int dtype, const void* x, int G, int R, int C, float* out, hipStream_t st);
+int sm_segment_mean_bwd(int dtype, const float* dy, int G, int R, int C, void* dx, hipStream_t st);
 
 /* ---- optimizer (train_ssl_mae.py:163 AdamW, :87-89 GradScaler inf-skip) */
 int sm_nonfinite(const float* g, int64_t n, int* flag, hipStream_t st);

@@ -739,7 +739,10 @@ static int gemm_run(int ab_dtype, int c_dtype, int a_layout, int b_layout, int M
                     float* colsum, float* colsum_out, hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
   if (ab_dtype == SM_BF16) {
-    if (K % 8 || lda % 8 || ldb % 8) return -2;
+    // a K-major operand is staged in 8-element (16-B) chunks along K: K % 8; M/N-major
+    // operands are staged one K row per chunk, so any K (e.g. the token-row reduction
+    // of a weight gradient over B * 49 rows) works
+    if (((a_layout == 0 || b_layout == 0) && K % 8) || lda % 8 || ldb % 8) return -2;
     if (a_layout == 1 && M % 8) return -2;
     if (b_layout == 1 && N % 8) return -2;
     if (((uintptr_t)A | (uintptr_t)B) & 15) return -2;

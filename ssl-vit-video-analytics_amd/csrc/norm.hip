@@ -298,7 +298,7 @@ struct ColMap {
 };
 
 template <typename T>
-__global__ __launch_bounds__(256) void bn_stats_kernel(const T* x, int64_t M, int C, int rows_per_block,
+__global__ __launch_bounds__(256) void bn_stats_kernel(const T* x, int64_t M, int C, int64_t ld, int rows_per_block,
                                                        float* part /*[nb][2][C]*/) {
   __shared__ float red[2][256 * 4];
   ColMap cm(C);
@@ -310,7 +310,7 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const T* x, int64_t M, in
   if (cm.active()) {
     for (int64_t row = r0 + cm.r; row < r1; row += cm.rpp) {
       float v[4];
-      load4(x + row * C + cm.chunk * 4, v);
+      load4(x + row * ld + cm.chunk * 4, v);
 #pragma unroll
       for (int j = 0; j < 4; ++j) { const float d = v[j] - shift[j]; s[j] += d; q[j] += d * d; }
     }
@@ -417,8 +417,9 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const TI* x, const float*
 template <typename TI, typename TD>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const TD* dy, const TI* x, const float* mean,
                                                             const float* rstd, const float* w, const float* b,
-                                                            int64_t M, int C, int rows_per_block, int gelu,
-                                                            const float* row_scale, int64_t rpg, float* part) {
+                                                            int64_t M, int C, int64_t ld, int rows_per_block,
+                                                            int gelu, const float* row_scale, int64_t rpg,
+                                                            float* part) {
   __shared__ float red[2][256 * 4];
   ColMap cm(C);
   float sg[4] = {0, 0, 0, 0}, sgx[4] = {0, 0, 0, 0};
@@ -433,8 +434,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const TD* dy, const 
     const int64_t r1 = min(M, r0 + rows_per_block);
     for (int64_t row = r0 + cm.r; row < r1; row += cm.rpp) {
       float xv[4], dv[4];
-      load4(x + row * C + cm.chunk * 4, xv);
-      load4(dy + row * C + cm.chunk * 4, dv);
+      load4(x + row * ld + cm.chunk * 4, xv);
+      load4(dy + row * ld + cm.chunk * 4, dv);
       const float rsc = row_scale ? row_scale[row / rpg] : 1.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -477,7 +478,7 @@ __global__ void bn_bwd_finalize_kernel(const double* sums /*[2][C]*/, int64_t M,
 template <typename TI, typename TD, typename TX>
 __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const TD* dy, const TI* x, const float* mean,
                                                         const float* rstd, const float* w, const float* b,
-                                                        const float* coef, TX* dx, int64_t M, int C,
+                                                        const float* coef, TX* dx, int64_t M, int C, int64_t ld,
                                                         int rows_per_block, int gelu, const float* row_scale,
                                                         int64_t rpg) {
   Col8 cm(C);
@@ -492,7 +493,7 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const TD* dy, const TI* 
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = min(M, r0 + rows_per_block);
   for (int64_t row = r0 + cm.r; row < r1; row += cm.rpp) {
-    const int64_t e = row * C + cm.chunk * 8;
+    const int64_t e = row * ld + cm.chunk * 8;
     float xv[8], dv[8], o[8];
     load8(x + e, xv);
     load8(dy + e, dv);
@@ -723,30 +724,68 @@ extern "C" int64_t sm_bn_workspace_bytes(int64_t M, int C) {
   return nb * 2 * C * 4 + 2 * C * 8 + 2 * C * 4 + 64;
 }
 
-// batch statistics -> mean/rstd (+ running-stat update `updates` times)
+// batch statistics -> mean/rstd (+ running-stat update `updates` times).  Channels
+// above 1024 (stage-4 MBConv, 1536) are processed in column slices of the same
+// [M][C] rows (row stride C).
+static const int BN_MAX_SLICE = 1024;
+
+static int bn_stats_slice(int x_dtype, int64_t M, int C, int64_t ld, const void* x, float* mean, float* rstd,
+                          float* run_mean, float* run_var, int64_t* nbt, float momentum, float eps, int updates,
+                          float* part, double* sums, hipStream_t st) {
+  const int rpb = red_rows_per_block(M, C);
+  const int nb = (int)((M + rpb - 1) / rpb);
+  if (x_dtype == SM_BF16) {
+    hipLaunchKernelGGL(bn_stats_kernel<__bf16>, dim3(nb), dim3(256), 0, st, (const __bf16*)x, M, C, ld, rpb, part);
+    colred(part, nb, 2 * C, sums, nullptr, 0, st);
+    hipLaunchKernelGGL(bn_finalize_kernel<__bf16>, dim3((C + 127) / 128), dim3(128), 0, st, sums,
+                       (const __bf16*)x, M, C, eps, momentum, mean, rstd, run_mean, run_var, updates, nbt);
+  } else {
+    hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(nb), dim3(256), 0, st, (const float*)x, M, C, ld, rpb, part);
+    colred(part, nb, 2 * C, sums, nullptr, 0, st);
+    hipLaunchKernelGGL(bn_finalize_kernel<float>, dim3((C + 127) / 128), dim3(128), 0, st, sums,
+                       (const float*)x, M, C, eps, momentum, mean, rstd, run_mean, run_var, updates, nbt);
+  }
+  return 0;
+}
+
 extern "C" int sm_bn_stats(int x_dtype, int64_t M, int C, const void* x, float* mean, float* rstd,
                            float* run_mean, float* run_var, int64_t* num_batches_tracked, float momentum, float eps,
                            int updates, void* ws, int64_t ws_bytes, hipStream_t st) {
   if (M <= 0) return -2;
-  if (C % 4 || C / 4 > 256) return -2;
+  if (C % 4 || C > 4 * BN_MAX_SLICE || (C > BN_MAX_SLICE && C % 8)) return -2;
   const int rpb = red_rows_per_block(M, C);
   const int nb = (int)((M + rpb - 1) / rpb);
   if (ws_bytes < (int64_t)nb * 2 * C * 4 + 2 * C * 8 + 8) return -4;
   float* part = (float*)ws;
   double* sums = (double*)(((uintptr_t)(part + (int64_t)nb * 2 * C) + 7) & ~(uintptr_t)7);
-  if (x_dtype == SM_BF16) {
-    hipLaunchKernelGGL(bn_stats_kernel<__bf16>, dim3(nb), dim3(256), 0, st, (const __bf16*)x, M, C, rpb, part);
-    colred(part, nb, 2 * C, sums, nullptr, 0, st);
-    hipLaunchKernelGGL(bn_finalize_kernel<__bf16>, dim3((C + 127) / 128), dim3(128), 0, st, sums,
-                       (const __bf16*)x, M, C, eps, momentum, mean, rstd, run_mean, run_var, updates,
-                       num_batches_tracked);
-  } else {
-    hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(nb), dim3(256), 0, st, (const float*)x, M, C, rpb, part);
-    colred(part, nb, 2 * C, sums, nullptr, 0, st);
-    hipLaunchKernelGGL(bn_finalize_kernel<float>, dim3((C + 127) / 128), dim3(128), 0, st, sums,
-                       (const float*)x, M, C, eps, momentum, mean, rstd, run_mean, run_var, updates,
-                       num_batches_tracked);
+  const int nsl = (C + BN_MAX_SLICE - 1) / BN_MAX_SLICE;
+  const int w = nsl == 1 ? C : (C / nsl + 7) / 8 * 8;
+  const size_t es = x_dtype == SM_BF16 ? 2 : 4;
+  for (int c0 = 0; c0 < C; c0 += w) {
+    const int cs = min(w, C - c0);
+    bn_stats_slice(x_dtype, M, cs, C, (const char*)x + c0 * es, mean + c0, rstd + c0,
+                   run_mean ? run_mean + c0 : nullptr, run_var ? run_var + c0 : nullptr,
+                   c0 == 0 ? num_batches_tracked : nullptr, momentum, eps, updates, part, sums, st);
   }
+  SM_CHECK_LAUNCH();
+  return 0;
+}
+
+// eval-mode BatchNorm (running statistics): mean = running_mean, rstd = 1/sqrt(var + eps),
+// in the form every BN consumer (bn_apply, the folded ChanAffine loads) takes
+__global__ void bn_eval_params_kernel(const float* run_mean, const float* run_var, int C, float eps, float* mean,
+                                      float* rstd) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  mean[c] = run_mean[c];
+  rstd[c] = 1.0f / sqrtf(run_var[c] + eps);
+}
+
+extern "C" int sm_bn_eval_params(const float* run_mean, const float* run_var, int C, float eps, float* mean,
+                                 float* rstd, hipStream_t st) {
+  if (C <= 0) return -2;
+  hipLaunchKernelGGL(bn_eval_params_kernel, dim3((C + 255) / 256), dim3(256), 0, st, run_mean, run_var, C, eps,
+                     mean, rstd);
   SM_CHECK_LAUNCH();
   return 0;
 }
@@ -792,24 +831,35 @@ extern "C" int sm_bn_bwd(int x_dtype, int g_dtype, int64_t M, int C, const void*
                          int64_t ws_bytes, hipStream_t st) {
   const int64_t rpg = rows_per_group > 0 ? rows_per_group : 1;
   if (M <= 0) return 0;
-  if (C % 8 || C / 4 > 256) return -2;
+  if (C % 8 || C > 4 * BN_MAX_SLICE) return -2;
   const int rpb = red_rows_per_block(M, C);
   const int nb = (int)((M + rpb - 1) / rpb);
   if (ws_bytes < (int64_t)nb * 2 * C * 4 + 2 * C * 8 + 2 * C * 4 + 8) return -4;
   float* part = (float*)ws;
   double* sums = (double*)(((uintptr_t)(part + (int64_t)nb * 2 * C) + 7) & ~(uintptr_t)7);
   float* coef = (float*)(sums + 2 * C);
-  DISPATCH2(x_dtype, g_dtype,
-            hipLaunchKernelGGL((bn_bwd_reduce_kernel<T1, T2>), dim3(nb), dim3(256), 0, st, (const T2*)dy,
-                               (const T1*)x, mean, rstd, w, b, M, C, rpb, gelu, row_scale, rpg, part));
-  colred(part, nb, 2 * C, sums, nullptr, 0, st);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 127) / 128), dim3(128), 0, st, sums, M, C, dw, db, coef);
   const int srpb = stream_rows_per_block(M);
   const int snb = (int)((M + srpb - 1) / srpb);
-  DISPATCH2(x_dtype, g_dtype,
-            hipLaunchKernelGGL((bn_bwd_dx_kernel<T1, T2, T2>), dim3(snb), dim3(256), 0, st,
-                               (const T2*)dy, (const T1*)x, mean, rstd, w, b, coef, (T2*)dx, M, C, srpb, gelu,
-                               row_scale, rpg));
+  const int nsl = (C + BN_MAX_SLICE - 1) / BN_MAX_SLICE;
+  const int wd = (C / nsl + 7) / 8 * 8;
+  const size_t xs = x_dtype == SM_BF16 ? 2 : 4, gs = g_dtype == SM_BF16 ? 2 : 4;
+  for (int c0 = 0; c0 < C; c0 += wd) {   // channel slices of <= 1024 over the same rows
+    const int cs = min(wd, C - c0);
+    const void* xo = (const char*)x + c0 * xs;
+    const void* dyo = (const char*)dy + c0 * gs;
+    void* dxo = (char*)dx + c0 * gs;
+    DISPATCH2(x_dtype, g_dtype,
+              hipLaunchKernelGGL((bn_bwd_reduce_kernel<T1, T2>), dim3(nb), dim3(256), 0, st, (const T2*)dyo,
+                                 (const T1*)xo, mean + c0, rstd + c0, w + c0, b + c0, M, cs, (int64_t)C, rpb, gelu,
+                                 row_scale, rpg, part));
+    colred(part, nb, 2 * cs, sums, nullptr, 0, st);
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((cs + 127) / 128), dim3(128), 0, st, sums, M, cs, dw + c0,
+                       db + c0, coef);
+    DISPATCH2(x_dtype, g_dtype,
+              hipLaunchKernelGGL((bn_bwd_dx_kernel<T1, T2, T2>), dim3(snb), dim3(256), 0, st,
+                                 (const T2*)dyo, (const T1*)xo, mean + c0, rstd + c0, w + c0, b + c0, coef, (T2*)dxo,
+                                 M, cs, (int64_t)C, srpb, gelu, row_scale, rpg));
+  }
   SM_CHECK_LAUNCH();
   return 0;
 }

@@ -70,11 +70,26 @@ def _done(*params):
     params[0]._sm_flat.done(*params)
 
 
+def _bn_params(a2d, bn, updates=1):
+    """(mean, rstd) of a BatchNorm2d: batch statistics in train mode (running stats
+    updated `updates` times), the running statistics in eval mode."""
+    if not bn.training:
+        return K.bn_eval_params(bn)
+    return K.bn_stats(a2d, bn.running_mean, bn.running_var, bn.momentum, bn.eps, updates, bn.num_batches_tracked)
+
+
 def _bn_forward(a2d, bn, gelu, residual=None, updates=1):
-    mean, rstd = K.bn_stats(a2d, bn.running_mean, bn.running_var, bn.momentum, bn.eps, updates,
-                            bn.num_batches_tracked)
+    mean, rstd = _bn_params(a2d, bn, updates)
     y = K.bn_apply(a2d, mean, rstd, bn.weight.detach(), bn.bias.detach(), gelu=gelu, residual=residual)
     return y, mean, rstd
+
+
+def _train_bn_only(ctx, *bns):
+    """The fused backward kernels differentiate through batch statistics; the
+    reference never backpropagates through eval-mode BatchNorm (train_finetune.py
+    trains under model.train() and evaluates under no_grad)."""
+    if not all(bn.training for bn in bns):
+        raise NotImplementedError("backward through eval-mode BatchNorm is not supported (train-mode BN only)")
 
 
 # ============================================================================ stem
@@ -106,6 +121,7 @@ class StemFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        _train_bn_only(ctx, ctx.st.bn1, ctx.st.bn2)
         clip, a1, a2, m1, r1, m2, r2, w1p, w2p = ctx.saved_tensors
         w1, g1, b1, w2, g2, b2 = ctx.params
         act = ctx.st.mode.act
@@ -156,11 +172,14 @@ class MBConvFn(torch.autograd.Function):
         if fused:
             # BN0 + GELU folded into the depthwise conv's loads, BN2 statistics produced
             # by it, BN2 + GELU folded into the SE reads: no act(a1) / act(a2) in HBM
-            m0, r0 = K.bn_stats(a1, st.bn0.running_mean, st.bn0.running_var, st.bn0.momentum, st.bn0.eps,
-                                st.bn_updates, st.bn0.num_batches_tracked)
+            m0, r0 = _bn_params(a1, st.bn0, st.bn_updates)
             act0 = (m0, r0, g0.detach(), b0.detach(), True)
-            a2, m2, r2 = K.dwconv_fused(a1, act0, w_dw.detach().view(mid, 9), Fr, H, Wd, mid, s, bn_out=st.bn2,
-                                        bn_updates=st.bn_updates)
+            if st.bn2.training:
+                a2, m2, r2 = K.dwconv_fused(a1, act0, w_dw.detach().view(mid, 9), Fr, H, Wd, mid, s,
+                                            bn_out=st.bn2, bn_updates=st.bn_updates)
+            else:
+                a2 = K.dwconv_fused(a1, act0, w_dw.detach().view(mid, 9), Fr, H, Wd, mid, s)
+                m2, r2 = K.bn_eval_params(st.bn2)
             act2 = (m2, r2, g2.detach(), b2.detach(), True)
             h3, pooled, h1se, gate = K.se_fwd(a2, Fr, Ho * Wo, mid, w_fc0.detach(), w_fc2.detach(), act=act2)
         else:
@@ -172,8 +191,7 @@ class MBConvFn(torch.autograd.Function):
             del h2
         a3 = K.linear(h3, W(w_proj, mode).view(Cout, mid))
         del h3
-        mean5, rstd5 = K.bn_stats(a3, st.bn5.running_mean, st.bn5.running_var, st.bn5.momentum, st.bn5.eps,
-                                  st.bn_updates, st.bn5.num_batches_tracked)
+        mean5, rstd5 = _bn_params(a3, st.bn5, st.bn_updates)
         out = K.bn_apply(a3, mean5, rstd5, g5.detach(), b5.detach(), residual=x2d if st.res else None,
                          row_scale=st.dp_scale, rows_per_group=Ho * Wo)
         m5, r5 = mean5, rstd5
@@ -187,6 +205,7 @@ class MBConvFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
+        _train_bn_only(ctx, ctx.st.bn0, ctx.st.bn2, ctx.st.bn5)
         x, a1, a2, a3, m0, r0, m2, r2, m5, r5, pooled, h1se, gate = ctx.saved_tensors
         w_exp, g0, b0, w_dw, g2, b2, w_fc0, w_fc2, w_proj, g5, b5 = ctx.params
         st = ctx.st

@@ -73,7 +73,7 @@ def linear_dw_bias(dy, x, grad_w, grad_b):
     whose n0 == 0 blocks also sum dy (sm_linear_dw_bias); fp32 (parity): two ops."""
     M, N = dy.shape
     K = x.shape[1]
-    if dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and M % 8 == 0 and N % 8 == 0 and K % 8 == 0:
+    if dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and N % 8 == 0 and K % 8 == 0:
         _chk(dy, x, grad_w, grad_b)
         nbytes = query("sm_linear_dw_bias_workspace_bytes", M, N, K)
         ws = _ws(nbytes, dy.device)
@@ -147,6 +147,18 @@ def bn_stats(x2d, running_mean=None, running_var=None, momentum=0.1, eps=1e-5, u
     ws = _ws(nbytes, x2d.device)
     call("sm_bn_stats", dt(x2d), M, C, ptr(x2d), ptr(mean), ptr(rstd), ptr(running_mean), ptr(running_var),
          ptr(num_batches), float(momentum), float(eps), int(updates), ptr(ws), nbytes, stream())
+    return mean, rstd
+
+
+def bn_eval_params(bn):
+    """(mean, rstd) of an eval-mode BatchNorm module from its running statistics."""
+    C = bn.running_mean.numel()
+    dev = bn.running_mean.device
+    _chk(bn.running_mean)
+    mean = torch.empty(C, dtype=torch.float32, device=dev)
+    rstd = torch.empty(C, dtype=torch.float32, device=dev)
+    call("sm_bn_eval_params", ptr(bn.running_mean), ptr(bn.running_var), C, float(bn.eps), ptr(mean), ptr(rstd),
+         stream())
     return mean, rstd
 
 
@@ -462,6 +474,26 @@ def std(x):
     ws = _ws(nbytes, x.device)
     call("sm_std", dt(x), ptr(x), x.numel(), ptr(out), ptr(ws), nbytes, stream())
     return out
+
+
+# ------------------------------------------------------------------ fine-tune head pooling
+def segment_mean(x, G, R, C):
+    """x [G*R, C] (or [G, R, C]) -> fp32 [G, C], mean over the R rows of each segment."""
+    _chk(x)
+    if not x.is_contiguous() or x.numel() != G * R * C:
+        raise _lib.KernelError("segment_mean needs a contiguous [G][R][C] tensor")
+    out = torch.empty((G, C), dtype=torch.float32, device=x.device)
+    call("sm_segment_mean", dt(x), ptr(x), G, R, C, ptr(out), stream())
+    return out
+
+
+def segment_mean_bwd(dy, G, R, C, dtype):
+    _chk(dy)
+    if dy.dtype != torch.float32 or not dy.is_contiguous():
+        raise _lib.KernelError("segment_mean_bwd takes the fp32 [G][C] gradient of segment_mean")
+    dx = torch.empty((G * R, C), dtype=dtype, device=dy.device)
+    call("sm_segment_mean_bwd", dt(dx), ptr(dy), G, R, C, ptr(dx), stream())
+    return dx
 
 
 # ------------------------------------------------------------------ optimizer

@@ -49,12 +49,13 @@ def make_flat(root: nn.Module, dev):
 def ensure_flat(root: nn.Module, mode: Mode):
     """Move every parameter of `root` into one flat device buffer (once), then
     mark the start of a forward (zero-on-first-backward, bf16 shadow refresh)."""
-    flat = getattr(root, "_sm_flat", None)
-    dev = next(root.parameters()).device
+    params = list(root.parameters())
+    dev = params[0].device
     if dev.type != "cuda":
         raise RuntimeError("ssl_mae_amd models run on the GPU only (move the model with .to('cuda'))")
-    if flat is None or flat.device != dev or any(getattr(p, "_sm_flat", None) is not flat
-                                                 for p in root.parameters()):
+    # a sub-module (e.g. the MAE's encoder run on its own) uses its parent's buffer
+    flat = getattr(params[0], "_sm_flat", None)
+    if flat is None or flat.device != dev or any(getattr(p, "_sm_flat", None) is not flat for p in params):
         flat = make_flat(root, dev)
     flat.begin_forward(mode.bf16)
     return flat

@@ -43,7 +43,7 @@ class FlatParams:
             p._sm_grad = self.grad[o:o + n].view(p.shape)
             p._sm_bf16 = self.shadow[o:o + n].view(p.shape)
             p._sm_flat = self
-            p.grad = p._sm_grad if i < self.n_attach else None
+            p.grad = p._sm_grad if i < self.n_attach and p.requires_grad else None
         # [0, used_end): parameters on the MAE path (stage-4 params are never used by
         # forward_stage3 and, as with the reference's grad-None, are never updated)
         self.used_end = self.offsets[self.n_attach - 1] + (self.params[self.n_attach - 1].numel() + ALIGN - 1) \
@@ -117,7 +117,8 @@ class FlatParams:
             self.touched.clear()
             self._reset_buckets()
             for p in self.params[:self.n_attach]:
-                p.grad = p._sm_grad
+                if p.requires_grad:
+                    p.grad = p._sm_grad
         for p in params:
             self.touched.add(id(p))
 

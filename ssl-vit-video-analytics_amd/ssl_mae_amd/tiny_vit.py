@@ -212,12 +212,16 @@ class TinyViT(nn.Module):
         only the memory/time trade changes.  (An MBConv in a resident stage still
         drops its 4x-wide expand output and recomputes that one GEMM.)"""
         resident = self.resident_stages
+        # Without autograd (frozen encoder, no_grad evaluation) the reference's
+        # non-reentrant checkpoint runs each stage's forward once and never recomputes
+        # it, so BatchNorm takes the batch once: plain forward here too.
+        grad = torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters()))
         if resident == "auto":
             resident = auto_resident_stages(x.shape[0], x.shape[1] * 2, mode.bf16, x.device) \
-                if self.use_checkpoint and self.training else ()
+                if self.use_checkpoint and self.training and grad else ()
         for i in range(n_stages):
             stage = self.stages[i]
-            if self.use_checkpoint and self.training:
+            if self.use_checkpoint and self.training and grad:
                 if i in resident:
                     x = stage.run(x, mode, resident=True)
                 else:
@@ -243,13 +247,17 @@ class TinyViT(nn.Module):
         t = self.tokens_stage3(x, mode)
         return t.permute(0, 3, 1, 2)
 
+    def tokens_all(self, x, mode):
+        """All four stages, channels-last: frames [N,3,H,W] (any strides) or a clip
+        [B,3,T,H,W] (frames b*T + t) -> [N, H/16, W/16, C4]."""
+        t = self.patch_embed.run(x, mode)
+        return self._run_stages(t, 4, mode)
+
     def forward(self, x):
         """All four stages (tiny_vit.py:178-186) -> [N, C4, H/16, W/16] (NCHW view)."""
         mode = self._mode()
         self._prepare(mode)
-        t = self.patch_embed.run(x, mode)
-        t = self._run_stages(t, 4, mode)
-        return t.permute(0, 3, 1, 2)
+        return self.tokens_all(x, mode).permute(0, 3, 1, 2)
 
 
 # Peak HBM of one MAE training step per frame (GiB, bf16, 224x224 frames, measured

@@ -577,3 +577,59 @@ def test_dropout_masks_fwd_bwd_consistent():
     vals = torch.unique(s)
     assert len(vals) == 2 and vals[0] == 0 and abs(vals[1].item() - 1 / 0.9) < 1e-6
     assert abs((s > 0).float().mean() - 0.9) < 0.02
+
+
+@pytest.mark.parametrize("M", [98, 49, 1001])
+def test_weight_grad_any_row_count(M):
+    """dW = dy^T x over a token-row count that is not a multiple of 8 (fine-tune
+    per-frame calls: B * 7 * 7 rows): both operands M/N-major, K tail zero-filled."""
+    dy = rnd(M, 576, dtype=torch.bfloat16, seed=140, scale=0.1)
+    x = rnd(M, 1536, dtype=torch.bfloat16, seed=141)
+    gw = torch.zeros(576, 1536, device=DEV)
+    gb = torch.zeros(576, device=DEV)
+    KK().linear_dw_bias(dy.to(DEV), x.to(DEV), gw, gb)
+    assert rel_err(gw, dy.float().t() @ x.float()) < 2e-2
+    assert rel_err(gb, dy.float().sum(0)) < 1e-4
+
+
+@pytest.mark.parametrize("C", [48, 1536])
+def test_batchnorm_eval_and_wide_channels(C):
+    """Eval-mode BN from running statistics (sm_bn_eval_params + bn_apply) and train-mode
+    statistics / backward at C = 1536 (stage-4 MBConv: column slices) vs F.batch_norm."""
+    kk = KK()
+    M = 2000
+    x = (rnd(M, C, seed=150) * 2 + 0.5).to(DEV)
+    w = (rnd(C, seed=151) * 0.1 + 1).to(DEV)
+    b = (rnd(C, seed=152) * 0.1).to(DEV)
+
+    class BN:
+        running_mean = (rnd(C, seed=153) * 0.3).to(DEV)
+        running_var = (rnd(C, seed=154).abs() + 0.5).to(DEV)
+        eps = 1e-5
+    m, r = kk.bn_eval_params(BN)
+    y = kk.bn_apply(x, m, r, w, b, gelu=True)
+    ref = F.gelu(F.batch_norm(x, BN.running_mean, BN.running_var, w, b, False, 0.1, 1e-5))
+    assert rel_err(y, ref) < 1e-5
+    xr = x.detach().clone().requires_grad_(True)
+    rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    yr = F.gelu(F.batch_norm(xr, rm, rv, w, b, True, 0.1, 1e-5))
+    dy = rnd(M, C, seed=155).to(DEV)
+    yr.backward(dy)
+    rm2, rv2 = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    mean, rstd = kk.bn_stats(x, rm2, rv2)
+    assert rel_err(rm2, rm) < 1e-5 and rel_err(rv2, rv) < 1e-5
+    assert rel_err(kk.bn_apply(x, mean, rstd, w, b, gelu=True), yr) < 1e-5
+    dw, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    dx = kk.bn_bwd(dy, x, mean, rstd, w, b, True, dw, db)
+    assert rel_err(dx, xr.grad) < 1e-4
+
+
+def test_segment_mean_fwd_bwd():
+    kk = KK()
+    G, R, C = 37, 49, 576
+    x = rnd(G * R, C, dtype=torch.bfloat16, seed=160).to(DEV)
+    out = kk.segment_mean(x, G, R, C)
+    assert rel_err(out, x.float().view(G, R, C).mean(1)) < 1e-5
+    dy = rnd(G, C, seed=161).to(DEV)
+    dx = kk.segment_mean_bwd(dy, G, R, C, torch.bfloat16)
+    assert rel_err(dx, (dy / R)[:, None, :].expand(G, R, C).reshape(G * R, C)) < 1e-2

@@ -57,3 +57,29 @@ def test_frame_index_rule():
     for total in (16, 17, 40):
         idx = O.frame_indices(total, 8, 2)
         assert len(idx) == 8 and np.all(np.diff(idx) == 2) and idx[-1] < total
+
+
+def test_finetune_checkpoint_bridge(tmp_path):
+    """load_pretrained_ssl (train_finetune.py:43-63) reads both the MAE driver's
+    encoder-only file (no prefix, train_ssl_mae.py:190-194) and an `encoder.`-prefixed
+    full state; the reference's loader silently skips the former."""
+    import torch
+    from ssl_mae_amd.finetune import VideoClassifier, load_pretrained_ssl
+    from ssl_mae_amd.mae_vit_adapter import TinyVideoMAE
+    from ssl_mae_amd.tiny_vit import tiny_vit_21m_variant
+    cfg = {"dataset": {"clip_len": 4, "image_size": 112},
+           "model": {"decoder_embed_dim": 384, "decoder_depth": 1, "decoder_num_heads": 6}}
+    torch.manual_seed(0)
+    mae = TinyVideoMAE(tiny_vit_21m_variant(img_size=112), cfg)
+    enc = mae.encoder.state_dict()
+    torch.save(enc, tmp_path / "encoder_ep10.pth")
+    torch.save({"model": mae.state_dict()}, tmp_path / "full.pth")
+    for f in ("encoder_ep10.pth", "full.pth"):
+        torch.manual_seed(1)
+        clf = VideoClassifier(101)
+        assert load_pretrained_ssl(clf, str(tmp_path / f))
+        got = clf.backbone.state_dict()
+        assert set(got) == set(enc)
+        for k, v in enc.items():
+            assert torch.equal(got[k], v), (f, k)
+    assert not load_pretrained_ssl(VideoClassifier(5), str(tmp_path / "missing.pth"))
