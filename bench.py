@@ -49,6 +49,12 @@ def parse():
                          "comma list, or 'none'; default: the model's auto policy")
     ap.add_argument("--probe", default="dec_attn_fwd",
                     help="kernel group timed with events for the roofline line")
+    ap.add_argument("--model", default="tiny", choices=["tiny", "small"],
+                    help="tiny: tiny_vit_21m_variant + 4-layer decoder (BASELINE C2); small: the build-defined "
+                         "ViT-Small of BASELINE C3 (depths 2,2,12,2 + 8-layer decoder, SURVEY.md H8)")
+    ap.add_argument("--workload", default="mae", choices=["mae", "finetune"],
+                    help="mae: MAE pretraining step (C2/C3); finetune: frozen-encoder linear-probe step "
+                         "(BASELINE C4: 16-frame 112x112 clips, batch 64)")
     return ap.parse_args()
 
 
@@ -131,8 +137,10 @@ class Probe:
 
 def resident_used(model, frames, S):
     from ssl_mae_amd.tiny_vit import auto_resident_stages
-    r = model.encoder.resident_stages
-    return auto_resident_stages(frames, S, True, torch.device("cuda")) if r == "auto" else r
+    enc = model.encoder
+    r = enc.resident_stages
+    return auto_resident_stages(frames, S, True, torch.device("cuda"), key=(tuple(enc.depths), enc._sm_dec_depth)) \
+        if r == "auto" else r
 
 
 def main():
@@ -155,9 +163,13 @@ def main():
     from ssl_mae_amd.optim import FusedAdamW, GradScaler
     from ssl_mae_amd.train_ssl_mae import build_model, train_step
 
+    if args.workload == "finetune":
+        return bench_finetune(args, rank, world, dev)
     B, T, S, r = args.batch, args.frames, args.size, args.mask_ratio
+    small = args.model == "small"
     cfg = {"dataset": {"clip_len": T, "image_size": S, "stride": 4, "train_split": "-"},
-           "model": {"decoder_embed_dim": 384, "decoder_depth": 4, "decoder_num_heads": 6},
+           "model": {"decoder_embed_dim": 384, "decoder_depth": 8 if small else 4, "decoder_num_heads": 6,
+                     "encoder": "tiny_vit_small_variant" if small else "tiny_vit_21m_variant"},
            "ssl": {"mask_ratio": r, "norm_pix_loss": True},
            "training": {"batch_size": B, "lr": 5e-4, "log_interval": 20}}
     torch.manual_seed(1234)
@@ -234,9 +246,9 @@ def main():
             tr = pmc_traffic(args.probe, B, T, S)
             if tr:
                 roof.update(tr)
-        step_tflops = value / world * TRAIN_TFLOP_PER_CLIP
+        step_tflops = value / world * TRAIN_TFLOP_PER_CLIP if not small else None
         cpu = None
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and world == 1 and not small:
             try:
                 cpu = cpu_baseline(T, S, r)
             except Exception as e:  # the baseline must not kill the bench line
@@ -246,19 +258,98 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 2),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (U[0,1) ImageNet-normalised clips in HBM; random-init weights)",
-            "config": {"workload": "BASELINE config 2: TinyViT-21M-variant MAE (stem+stages 1-3) + 4x384 decoder, "
-                                   "T=8, 224x224, mask 0.75, bf16 autocast",
-                       "model": "tiny_vit_21m_variant + TinyVideoMAE", "global_batch": B * world,
+            "config": {"workload": ("BASELINE config 3: build-defined ViT-Small MAE (TinyViT depths 2,2,12,2, "
+                                    "stem+stages 1-3) + 8x384 decoder" if small else
+                                    "BASELINE config 2: TinyViT-21M-variant MAE (stem+stages 1-3) + 4x384 decoder")
+                                   + ", T=8, 224x224, mask 0.75, bf16 autocast",
+                       "model": ("tiny_vit_small_variant" if small else "tiny_vit_21m_variant") + " + TinyVideoMAE",
+                       "global_batch": B * world,
                        "per_gpu_batch": B, "frames": T, "image_size": S, "mask_ratio": r,
                        "parallelism": f"dp{world}",
                        "resident_stages": list(resident_used(model, B * T, S))},
             "roofline": roof,
-            "model_tflops_per_gpu": round(step_tflops, 1),
-            "model_mfu": round(step_tflops / MFMA_BF16_PEAK_TFLOPS, 4),
+            "model_tflops_per_gpu": round(step_tflops, 1) if step_tflops else None,
+            "model_mfu": round(step_tflops / MFMA_BF16_PEAK_TFLOPS, 4) if step_tflops else None,
             "peak_mem_gib": round(peak_mem, 1),
             "loss_first_last": [round(loss_vals[0], 5), round(loss_vals[-1], 5)],
             "cpu_baseline": cpu,
         }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def bench_finetune(args, rank, world, dev):
+    """BASELINE config 4: the linear-probe training step of train_finetune.py
+    (:84-124, mode linear_probe :294-296): VideoClassifier with the frozen HIP TinyViT
+    encoder (all four stages, train-mode BatchNorm per frame call as the reference),
+    temporal mean, Linear head, CE loss, AdamW on the head; bf16 autocast.  Batch 64
+    clips (configs/finetune.yaml) of 16 frames at 112x112.  Also times the evaluation
+    forward (model.eval(), no_grad)."""
+    from ssl_mae_amd.finetune import VideoClassifier, set_requires_grad
+    from ssl_mae_amd.init_rule import IMAGENET_MEAN, IMAGENET_STD
+    B, T, S, NC = 64, 16, 112, 101
+    torch.manual_seed(1234)
+    model = VideoClassifier(NC, img_size=S).to(dev)
+    set_requires_grad(model.backbone, False)
+    opt = torch.optim.AdamW([p for p in model.parameters() if p.requires_grad], lr=1e-4, weight_decay=0.01)
+    g = torch.Generator(device=dev).manual_seed(99 + rank)
+    mean = torch.tensor(IMAGENET_MEAN, device=dev).view(1, 3, 1, 1, 1)
+    std = torch.tensor(IMAGENET_STD, device=dev).view(1, 3, 1, 1, 1)
+    clip = (torch.rand(B, 3, T, S, S, generator=g, device=dev) - mean) / std
+    label = torch.randint(0, NC, (B,), generator=g, device=dev)
+    ce = torch.nn.CrossEntropyLoss()
+
+    def train_step():
+        model.train()
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            logits = model(clip)
+        loss = ce(logits.float(), label)
+        loss.backward()
+        opt.step()
+        return loss
+
+    def timed(fn, steps, warmup):
+        for _ in range(warmup):
+            fn()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            out = fn()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = t.item()
+        return el, out
+
+    el, loss = timed(train_step, args.steps, args.warmup)
+
+    def eval_step():
+        model.eval()
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+            return model(clip)
+    el_eval, _ = timed(eval_step, args.steps, 1)
+    if rank == 0:
+        value = B * world * args.steps / el
+        line = {"metric": "clips/sec (16x3x112x112) frozen-encoder fine-tune step (linear probe)",
+                "value": round(value, 3), "unit": "clips/s", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 2), "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+                "data": "synthetic (U[0,1) ImageNet-normalised clips in HBM; random-init weights)",
+                "config": {"workload": "BASELINE config 4: VideoClassifier(frozen TinyViT-21M-variant encoder, all 4 "
+                                       "stages, train-mode BN per frame call) + Linear(576, 101), CE + AdamW on "
+                                       "the head, T=16, 112x112, bf16 autocast",
+                           "global_batch": B * world, "per_gpu_batch": B, "frames": T, "image_size": S,
+                           "parallelism": f"dp{world}"},
+                "eval_clips_per_s": round(B * world * args.steps / el_eval, 2),
+                "loss_last": round(float(loss.item()), 5),
+                "peak_mem_gib": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1)}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -34,8 +34,15 @@ import torch
 import torch.nn.functional as F
 
 EMBED = (96, 192, 384, 576)
-DEPTHS = (2, 2, 6, 2)
+DEPTHS = (2, 2, 6, 2)          # tiny_vit_21m_variant (tiny_vit.py:188-191)
 HEADS = (3, 6, 12, 18)
+# BASELINE config 3 "ViT-Small": build-defined, the reference's
+# parametric TinyViT (tiny_vit.py:137-140) with depths (2, 2, 12, 2), decoder depth 8
+SMALL_DEPTHS = (2, 2, 12, 2)
+
+
+def depths_of(cfg):
+    return tuple(cfg.get("model", {}).get("depths", DEPTHS)) if cfg else DEPTHS
 
 
 # ---------------------------------------------------------------- masking / target
@@ -133,7 +140,7 @@ def _vit_block(P, pre, x, heads):
     return t.transpose(1, 2).reshape(N, C, H, W)
 
 
-def forward_stage3(P, x, trk=None, prefix="encoder.", acts=None):
+def forward_stage3(P, x, trk=None, prefix="encoder.", acts=None, depths=DEPTHS):
     pe = prefix + "patch_embed.patch_embed"
     h = F.gelu(_conv_bn(P, pe + ".0", x, 2, 1, trk=trk, updates=1))
     h = _conv_bn(P, pe + ".2", h, 1, 1, trk=trk, updates=1)
@@ -145,7 +152,7 @@ def forward_stage3(P, x, trk=None, prefix="encoder.", acts=None):
         if i > 0:
             h = _mbconv(P, sp + "0", h, EMBED[i - 1], EMBED[i], 2, trk, 2)
             j0 = 1
-        for j in range(DEPTHS[i]):
+        for j in range(depths[i]):
             if i == 0:
                 h = _mbconv(P, sp + str(j0 + j), h, EMBED[0], EMBED[0], 1, trk, 2)
             else:
@@ -173,7 +180,7 @@ def mae_forward(P, clip, mask, cfg, trk=None, acts=None):
     """TinyVideoMAE.forward (mae_vit_adapter.py:75-117) -> pred [B, T*L, 192]."""
     B, C, T, H, W = clip.shape
     frames = clip.permute(0, 2, 1, 3, 4).reshape(B * T, C, H, W)
-    lat = forward_stage3(P, frames, trk, acts=acts)
+    lat = forward_stage3(P, frames, trk, acts=acts, depths=depths_of(cfg))
     Lp = lat.shape[2] * lat.shape[3]
     tok = lat.flatten(2).transpose(1, 2)
     x = tok @ P["enc_to_dec.weight"].t() + P["enc_to_dec.bias"]
@@ -231,7 +238,7 @@ def param_shapes(cfg):
         if i > 0:
             mbconv(f"encoder.stages.{i}.0", EMBED[i - 1], EMBED[i])
             j = 1
-        for k in range(DEPTHS[i]):
+        for k in range(depths_of(cfg)[i]):
             if i == 0:
                 mbconv(f"encoder.stages.{i}.{j + k}", EMBED[0], EMBED[0])
             else:

@@ -102,6 +102,7 @@ class TinyVideoMAE(nn.Module):
         self.decoder_norm = nn.LayerNorm(self.decoder_embed_dim)
         self.decoder_pred = nn.Linear(self.decoder_embed_dim, self.patch_size ** 2 * 3, bias=True)
         self._mae = True
+        encoder._sm_dec_depth = self.decoder_depth
         self.initialize_weights()
         from .tiny_vit import index_modules
         index_modules(self)

@@ -179,6 +179,8 @@ class TinyViT(nn.Module):
         # (auto_resident_stages: as many as the device memory holds).
         self.resident_stages = "auto"
         self.embed_dims = list(embed_dims)
+        self.depths = list(depths)
+        self._sm_dec_depth = 4          # set by TinyVideoMAE (memory policy key)
         self.patch_embed = PatchEmbed(in_chans, embed_dims[0])
         self.stages = nn.ModuleList()
         dpr = [x.item() for x in torch.linspace(0, drop_path_rate, sum(depths))]
@@ -217,7 +219,8 @@ class TinyViT(nn.Module):
         # it, so BatchNorm takes the batch once: plain forward here too.
         grad = torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters()))
         if resident == "auto":
-            resident = auto_resident_stages(x.shape[0], x.shape[1] * 2, mode.bf16, x.device) \
+            resident = auto_resident_stages(x.shape[0], x.shape[1] * 2, mode.bf16, x.device,
+                                            key=(tuple(self.depths), self._sm_dec_depth)) \
                 if self.use_checkpoint and self.training and grad else ()
         for i in range(n_stages):
             stage = self.stages[i]
@@ -261,18 +264,24 @@ class TinyViT(nn.Module):
 
 
 # Peak HBM of one MAE training step per frame (GiB, bf16, 224x224 frames, measured
-# with bench.py at B=256 clips x T=8 on MI355X) for each resident-stage policy;
-# activations scale with the pixel count, fp32 doubles them.
-_PEAK_GIB_PER_FRAME = {(1, 2): 216.0 / 2048, (2,): 171.9 / 2048, (): 143.6 / 2048}
+# with bench.py at B=256 clips x T=8 on MI355X) for each resident-stage policy, per
+# (encoder depths, decoder depth); activations scale with the pixel count, fp32
+# doubles them.  An unlisted model takes the reference's policy (all checkpointed).
+_PEAK_GIB_PER_FRAME = {
+    ((2, 2, 6, 2), 4): {(1, 2): 216.0 / 2048, (2,): 171.9 / 2048, (): 143.6 / 2048},
+}
 
 
-def auto_resident_stages(frames, image_size, bf16, device, budget=0.85):
+def auto_resident_stages(frames, image_size, bf16, device, budget=0.85, key=((2, 2, 6, 2), 4)):
     """The largest resident set whose predicted step peak fits `budget` of the
     device memory (stage 0, the 112x112 MBConvs, is always recomputed)."""
+    table = _PEAK_GIB_PER_FRAME.get(key)
+    if table is None:
+        return ()
     total = torch.cuda.get_device_properties(device).total_memory / 2 ** 30
     scale = frames * (image_size / 224.0) ** 2 * (1 if bf16 else 2)
     for policy in ((1, 2), (2,)):
-        if _PEAK_GIB_PER_FRAME[policy] * scale <= budget * total:
+        if policy in table and table[policy] * scale <= budget * total:
             return policy
     return ()
 
@@ -287,3 +296,16 @@ def tiny_vit_21m_variant(img_size=112, use_checkpoint=True, **kwargs):
     """tiny_vit.py:188-191."""
     return TinyViT(img_size=img_size, embed_dims=[96, 192, 384, 576], depths=[2, 2, 6, 2],
                    num_heads=[3, 6, 12, 18], use_checkpoint=use_checkpoint, **kwargs)
+
+
+def tiny_vit_small_variant(img_size=112, use_checkpoint=True, **kwargs):
+    """BASELINE config 3 "ViT-Small" MAE encoder.  The reference has no Small model
+    (SURVEY.md H8); this is the build-defined variant of the reference's parametric
+    TinyViT (tiny_vit.py:137-140) that keeps the stage-3 width TinyVideoMAE hard-codes
+    (encoder_dim = 384, mae_vit_adapter.py:18): depths (2, 2, 12, 2) instead of
+    (2, 2, 6, 2); pair it with decoder_depth 8 in the MAE config."""
+    return TinyViT(img_size=img_size, embed_dims=[96, 192, 384, 576], depths=[2, 2, 12, 2],
+                   num_heads=[3, 6, 12, 18], use_checkpoint=use_checkpoint, **kwargs)
+
+
+ENCODERS = {"tiny_vit_21m_variant": tiny_vit_21m_variant, "tiny_vit_small_variant": tiny_vit_small_variant}

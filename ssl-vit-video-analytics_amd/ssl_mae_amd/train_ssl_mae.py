@@ -27,7 +27,7 @@ from .checkpoint import load_training_state, save_training_state
 from .mae_loader import ClipNormalizer, LazyVideoMAEDataset, collate_frames, tube_mask_with_index
 from .mae_vit_adapter import TinyVideoMAE
 from .optim import FusedAdamW, GradScaler
-from .tiny_vit import tiny_vit_21m_variant
+from .tiny_vit import ENCODERS
 from .utils import load_config, save_checkpoint, set_seed
 
 
@@ -113,7 +113,10 @@ def train_one_epoch(model, loader, optimizer, scaler, epoch, device, config, wri
 
 
 def build_model(cfg, device="cuda"):
-    encoder = tiny_vit_21m_variant(img_size=cfg["dataset"]["image_size"], use_checkpoint=True)
+    """train_ssl_mae.py:143-144; `model.encoder` may name the build-defined
+    "tiny_vit_small_variant" (BASELINE C3) instead of the reference's encoder."""
+    make = ENCODERS[cfg.get("model", {}).get("encoder", "tiny_vit_21m_variant")]
+    encoder = make(img_size=cfg["dataset"]["image_size"], use_checkpoint=True)
     return TinyVideoMAE(encoder, cfg).to(device)
 
 

@@ -131,11 +131,15 @@ def make_config(T, S, ratio, depth=4, dim=384, heads=6, batch=2):
     }
 
 
-def run_case(ref, name, B, T, S, ratio, steps, record_acts=True, clip_seed=1234):
+def run_case(ref, name, B, T, S, ratio, steps, record_acts=True, clip_seed=1234, depths=None, dec_depth=4):
     tiny_vit, adapter, mae_loader, ref_utils, tr = ref
     torch.set_num_threads(8)
-    cfg = make_config(T, S, ratio, batch=B)
-    encoder = tiny_vit.tiny_vit_21m_variant(img_size=S, use_checkpoint=True)
+    cfg = make_config(T, S, ratio, batch=B, depth=dec_depth)
+    if depths is None:
+        encoder = tiny_vit.tiny_vit_21m_variant(img_size=S, use_checkpoint=True)
+    else:   # build-defined "ViT-Small" (SURVEY.md H8): the reference's parametric TinyViT
+        encoder = tiny_vit.TinyViT(img_size=S, embed_dims=[96, 192, 384, 576], depths=list(depths),
+                                   num_heads=[3, 6, 12, 18], use_checkpoint=True)
     model = adapter.TinyVideoMAE(encoder, cfg)
     apply_rule(model)
     _parity_mode(model)
@@ -174,6 +178,8 @@ def run_case(ref, name, B, T, S, ratio, steps, record_acts=True, clip_seed=1234)
         h.remove()
 
     rec["B"], rec["T"], rec["S"], rec["ratio"], rec["steps"] = B, T, S, ratio, steps
+    rec["depths"] = np.array(depths if depths is not None else (2, 2, 6, 2))
+    rec["decoder_depth"] = dec_depth
     rec["clip_seed"] = clip_seed
     rec["avg_loss"] = np.float64(avg_loss)
     rec["mask"] = torch.stack(masks).numpy()
@@ -235,6 +241,25 @@ def patchify_case(ref):
     print("wrote", out)
 
 
+def init_case(ref):
+    """A17: the reference's own initialisation under set_seed(42) -- TinyVideoMAE(
+    tiny_vit_21m_variant(112), ssl_mae.yaml shapes) built exactly as main() builds it
+    (train_ssl_mae.py:131,143-144) -- recorded as per-parameter checksums."""
+    tiny_vit, adapter, _, ref_utils, _ = ref
+    cfg = make_config(16, 112, 0.9)
+    ref_utils.set_seed(42)
+    model = adapter.TinyVideoMAE(tiny_vit.tiny_vit_21m_variant(img_size=112, use_checkpoint=True), cfg)
+    rec = {}
+    for n, p in model.named_parameters():
+        v = p.detach().double().numpy().ravel()
+        rec["sum/" + n] = np.float64(v.sum())
+        rec["sumsq/" + n] = np.float64((v * v).sum())
+        rec["head/" + n] = v[:8].astype(np.float32)
+    out = os.path.join(HERE, "init_seed42.npz")
+    np.savez_compressed(out, **rec)
+    print("wrote", out)
+
+
 if __name__ == "__main__":
     ref = _import_reference()
     masks_case(ref)
@@ -242,5 +267,10 @@ if __name__ == "__main__":
     run_case(ref, "step_b2_t2_s32", B=2, T=2, S=32, ratio=0.75, steps=1)
     run_case(ref, "step2_b2_t2_s32", B=2, T=2, S=32, ratio=0.75, steps=2)
     run_case(ref, "step_b2_t4_s64", B=2, T=4, S=64, ratio=0.9, steps=1)
+    if "--small" in sys.argv or "--all" in sys.argv:
+        run_case(ref, "step_small_b2_t2_s32", B=2, T=2, S=32, ratio=0.75, steps=1, depths=(2, 2, 12, 2),
+                 dec_depth=8)
+    if "--init" in sys.argv or "--all" in sys.argv:
+        init_case(ref)
     if "--full" in sys.argv:
         run_case(ref, "step_b1_t8_s224", B=1, T=8, S=224, ratio=0.75, steps=1)

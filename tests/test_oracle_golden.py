@@ -10,12 +10,14 @@ import torch
 from oracle import mae_oracle as O
 from ssl_mae_amd.init_rule import param_value, synthetic_clip
 
-STEP_CASES = ["step_b2_t2_s32", "step_b2_t4_s64", "step_b1_t8_s224"]
+STEP_CASES = ["step_b2_t2_s32", "step_b2_t4_s64", "step_b1_t8_s224", "step_small_b2_t2_s32"]
 
 
 def _cfg(d):
+    depths = tuple(int(v) for v in d["depths"]) if "depths" in d.files else O.DEPTHS
+    dec = int(d["decoder_depth"]) if "decoder_depth" in d.files else 4
     return {"dataset": {"clip_len": int(d["T"]), "image_size": int(d["S"])},
-            "model": {"decoder_embed_dim": 384, "decoder_depth": 4, "decoder_num_heads": 6},
+            "model": {"decoder_embed_dim": 384, "decoder_depth": dec, "decoder_num_heads": 6, "depths": depths},
             "ssl": {"mask_ratio": float(d["ratio"]), "norm_pix_loss": True}}
 
 
@@ -132,3 +134,24 @@ def test_two_steps_match_reference(golden_dir):
         atol = np.where(np.abs(gh[: p.numel()]) < 1e-6, 2 * 2.1 * 5e-4, 2e-5)
         ok, e = _close(p.reshape(-1)[:8].numpy(), d["param_head/" + name], 1e-5, atol)
         assert ok, (name, e)
+
+
+def test_reference_init_under_seed42(golden_dir):
+    """A17: TinyVideoMAE(tiny_vit_21m_variant(112)) built under set_seed(42) exactly as
+    the reference's main() builds it (train_ssl_mae.py:131,143-144) gives the
+    reference's initial parameters bit for bit (same modules, same init calls, same
+    RNG consumption: mae_vit_adapter.py:57-73, tiny_vit.py:17-18,49)."""
+    from ssl_mae_amd.mae_vit_adapter import TinyVideoMAE
+    from ssl_mae_amd.tiny_vit import tiny_vit_21m_variant
+    from ssl_mae_amd.utils import set_seed
+    d = np.load(os.path.join(golden_dir, "init_seed42.npz"))
+    cfg = {"dataset": {"clip_len": 16, "image_size": 112},
+           "model": {"decoder_embed_dim": 384, "decoder_depth": 4, "decoder_num_heads": 6}}
+    set_seed(42)
+    model = TinyVideoMAE(tiny_vit_21m_variant(img_size=112, use_checkpoint=True), cfg)
+    names = [n for n, _ in model.named_parameters()]
+    assert sorted(names) == sorted(k[4:] for k in d.files if k.startswith("sum/"))
+    for n, p in model.named_parameters():
+        v = p.detach().double().numpy().ravel()
+        assert np.array_equal(v[:8].astype(np.float32), d["head/" + n]), n
+        assert v.sum() == float(d["sum/" + n]) and (v * v).sum() == float(d["sumsq/" + n]), n
