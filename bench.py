@@ -47,8 +47,9 @@ def parse():
     ap.add_argument("--resident", default="",
                     help="encoder stages kept resident in HBM (no checkpoint recompute): "
                          "comma list, or 'none'; default: the model's auto policy")
-    ap.add_argument("--probe", default="dec_attn_fwd",
-                    help="kernel group timed with events for the roofline line")
+    ap.add_argument("--probe", default="dec_attn_bwd",
+                    help="kernel group timed with events for the roofline line: dec_attn_bwd (the top-time "
+                         "kernels of the step: decoder attention dK/dV + dQ) or dec_attn_fwd")
     ap.add_argument("--model", default="tiny", choices=["tiny", "small"],
                     help="tiny: tiny_vit_21m_variant + 4-layer decoder (BASELINE C2); small: the build-defined "
                          "ViT-Small of BASELINE C3 (depths 2,2,12,2 + 8-layer decoder, SURVEY.md H8)")
@@ -81,26 +82,34 @@ def cpu_baseline(T, S, ratio):
                       f"(dropout off) on {threads} host threads; {dt:.1f} s"}
 
 
-PROBE_KERNELS = {"dec_attn_fwd": "attn_fwd_bf16<64, true>"}
+PROBE_KERNELS = {"dec_attn_fwd": "attn_fwd_bf16<64, true>",
+                 "dec_attn_bwd": "attn_bwd_dq_bf16<64, true>+attn_bwd_dkdv_bf16<64, true>"}
+REFERENCE_CPU = {"value": 0.036, "unit": "clips/s", "cores": 8, "kind": "reference",
+                 "sample": "the reference's train_one_epoch path itself (fp32, dropout/DropPath on) at BASELINE "
+                           "config 1 (B=4, T=8, 224x224, mask 0.75): 102.5 / 110.7 s per step on the 8 Xeon "
+                           "cores of the build container (SURVEY.md §8(d)); the reference cannot travel to the "
+                           "GPU box"}
 
 
 def pmc_traffic(probe, B, T, S):
-    """HBM bytes per launch of the probe kernel, measured with PMC counters by
+    """HBM bytes per launch of the probe kernel(s), measured with PMC counters by
     scripts/pmc_traffic.sh (FETCH_SIZE / WRITE_SIZE passes over this bench at the
     default workload) and committed as profiles/*_traffic.json; None if absent."""
     import glob
     if (B, T, S) != (256, 8, 224):
         return None
+    L = T * (S // 8) ** 2
+    qkv, o, lse = B * L * 3 * 384 * 2, B * L * 384 * 2, B * 6 * L * 4
+    algo = {"dec_attn_fwd": qkv + o + lse,                       # qkv read + O write + lse
+            "dec_attn_bwd": qkv + 2 * o + lse + qkv}             # qkv, O, dO, lse read + dqkv write
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), reverse=True):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
         if d.get("kernel") == PROBE_KERNELS.get(probe):
-            L = T * (S // 8) ** 2
-            algo = B * L * (3 * 384 + 384) * 2 + B * 6 * L * 4    # qkv read + O write (bf16) + lse
             return {"traffic": round(d["traffic_bytes"] / 1e9, 3), "traffic_unit": "GB/launch",
-                    "algorithmic_gb_per_launch": round(algo / 1e9, 3),
+                    "algorithmic_gb_per_launch": round(algo[probe] / 1e9, 3),
                     "traffic_source": os.path.relpath(f, ROOT)}
     return None
 
@@ -187,6 +196,9 @@ def main():
     clips = [((torch.rand(B, 3, T, S, S, generator=g, device=dev) - mean) / std) for _ in range(2)]
 
     probe = Probe(args.probe)
+    stem_probe = Probe("patch_embed_fwd")
+    from ssl_mae_amd import tiny_vit as TV
+    stem_probe.wrap(TV.PatchEmbed, "run", lambda *a, **k: True)
     Ld = T * (S // 8) ** 2
     if args.probe == "dec_attn_fwd":
         probe.wrap(K, "attn_fwd", lambda qkv, N, L, H, D, *a, **k: D == 64 and L == Ld)
@@ -213,6 +225,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     probe.active = True
+    stem_probe.active = True
     t0 = time.perf_counter()
     losses = []
     for i in range(args.steps):
@@ -220,6 +233,7 @@ def main():
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     probe.active = False
+    stem_probe.active = False
     if world > 1:
         dist.barrier()
     elapsed = t1 - t0
@@ -246,6 +260,17 @@ def main():
             tr = pmc_traffic(args.probe, B, T, S)
             if tr:
                 roof.update(tr)
+        savg = stem_probe.avg_ms()
+        if roof is not None and savg:
+            # north star: achieved HBM GB/s of the patch-embed stem (forward launch:
+            # conv1 + BN + GELU + conv2 + BN), algorithmic bytes SURVEY.md §8(d):
+            # fp32 clip in (3*T*H*W*4) + bf16 [frames,112,112,96] out = 24.1 MB/clip
+            sbytes = B * (3 * T * S * S * 4 + 96 * T * (S // 2) * (S // 2) * 2)
+            roof["patch_embed"] = {"bound": "hbm", "achieved": round(sbytes / (savg * 1e-3) / 1e9, 1),
+                                   "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                   "frac": round(sbytes / (savg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                   "algorithmic_gb_per_launch": round(sbytes / 1e9, 3),
+                                   "avg_launch_ms": round(savg, 3), "launches": len(stem_probe.pairs)}
         step_tflops = value / world * TRAIN_TFLOP_PER_CLIP if not small else None
         cpu = None
         if not args.no_cpu_baseline and world == 1 and not small:
@@ -273,6 +298,7 @@ def main():
             "peak_mem_gib": round(peak_mem, 1),
             "loss_first_last": [round(loss_vals[0], 5), round(loss_vals[-1], 5)],
             "cpu_baseline": cpu,
+            "cpu_baseline_reference": REFERENCE_CPU if not small else None,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

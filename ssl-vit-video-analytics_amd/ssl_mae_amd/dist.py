@@ -24,7 +24,7 @@ import os
 import torch
 import torch.distributed as dist
 
-from . import kernels as K
+from . import ops as K    # every kernel launch through the torch.ops.ssl_mae dispatcher
 
 BUCKET_ELEMS = 6 * 1024 * 1024   # 24 MiB fp32 per collective
 

@@ -32,7 +32,7 @@ import random
 import torch
 import torch.distributed as dist
 
-from . import kernels as K
+from . import ops as K    # every kernel launch through the torch.ops.ssl_mae dispatcher
 
 
 def _is_float_tensor(t):

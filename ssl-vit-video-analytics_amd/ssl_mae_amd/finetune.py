@@ -29,7 +29,7 @@ import os
 import torch
 import torch.nn as nn
 
-from . import kernels as K
+from . import ops as K    # every kernel launch through the torch.ops.ssl_mae dispatcher
 from .functions import Mode
 from .mae_vit_adapter import ensure_flat, next_seed_base
 from .tiny_vit import TinyViT

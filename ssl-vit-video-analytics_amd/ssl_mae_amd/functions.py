@@ -20,7 +20,7 @@ import math
 
 import torch
 
-from . import kernels as K
+from . import ops as K    # every kernel launch through the torch.ops.ssl_mae dispatcher
 
 
 class Mode:

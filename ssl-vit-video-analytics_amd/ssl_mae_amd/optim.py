@@ -16,7 +16,7 @@ a host sync.
 """
 import torch
 
-from . import kernels as K
+from . import ops as K    # every kernel launch through the torch.ops.ssl_mae dispatcher
 
 ALIGN = 8  # elements: keeps every bf16 view 16-byte aligned
 

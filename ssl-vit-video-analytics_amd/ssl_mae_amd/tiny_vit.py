@@ -13,7 +13,7 @@ import torch
 import torch.nn as nn
 import torch.utils.checkpoint as checkpoint
 
-from . import kernels as K
+from . import ops as K    # every kernel launch through the torch.ops.ssl_mae dispatcher
 from .functions import BlockFn, MBConvFn, Mode, StemFn
 
 
@@ -269,6 +269,8 @@ class TinyViT(nn.Module):
 # doubles them.  An unlisted model takes the reference's policy (all checkpointed).
 _PEAK_GIB_PER_FRAME = {
     ((2, 2, 6, 2), 4): {(1, 2): 216.0 / 2048, (2,): 171.9 / 2048, (): 143.6 / 2048},
+    # C3 ViT-Small (depths 2,2,12,2 + 8-layer decoder): (2,) and (1, 2) exceed 288 GB at B=256
+    ((2, 2, 12, 2), 8): {(): 184.0 / 2048},
 }
 
 

@@ -21,7 +21,7 @@ from pathlib import Path
 
 import torch
 
-from . import kernels as K
+from . import ops as K    # every kernel launch through the torch.ops.ssl_mae dispatcher
 from .functions import mae_loss, masked_pred_std
 from .checkpoint import load_training_state, save_training_state
 from .mae_loader import ClipNormalizer, LazyVideoMAEDataset, collate_frames, tube_mask_with_index

@@ -33,3 +33,35 @@ def test_no_cpu_fallback():
     from ssl_mae_amd import kernels
     with pytest.raises(Exception):
         kernels.layernorm(torch.zeros(4, 8), torch.ones(8), torch.zeros(8))
+
+
+def test_torch_library_registration():
+    """Every compute entry point of the C ABI is a torch.ops.ssl_mae operator with a
+    schema (SURVEY.md §8(b) Registration); workspace / partial-size queries stay
+    host-side.  Fake (meta) implementations propagate shapes without a GPU."""
+    import torch
+    from torch._subclasses.fake_tensor import FakeTensorMode
+    from ssl_mae_amd import _lib, ops
+    registered = set(ops.registered_ops())
+    alias = {"layernorm_fwd": "layernorm", "dwconv_fwd": "dwconv", "gelu_fwd": "gelu", "fill": "fill_",
+             "scale": "scale_", "dwconv_fused_fwd": "dwconv_fused", "pos_blend_fwd": "pos_blend"}
+    internal = {"add",                       # not used by the step
+                "bn_stats_from_partials"}    # the statistics step inside ssl_mae::dwconv_fused
+    for sym in _lib.exported_symbols():
+        base = sym[3:]
+        if base.endswith(("_workspace_bytes", "_partial_rows")) or base in internal:
+            continue                          # host-side sizing queries
+        name = alias.get(base, base)
+        assert name in registered, (sym, name)
+        assert str(getattr(torch.ops.ssl_mae, name).default._schema).startswith("ssl_mae::" + name)
+    with FakeTensorMode():
+        qkv = torch.empty(2 * 784, 3 * 384, dtype=torch.bfloat16)
+        o, lse = ops.attn_fwd(qkv, 2, 784, 12, 32, 0.1, 123)
+        assert o.shape == (2 * 784, 384) and lse.shape == (2, 12, 784)
+        y, pre = ops.linear(torch.empty(64, 384, dtype=torch.bfloat16), torch.empty(1536, 384, dtype=torch.bfloat16),
+                            torch.empty(1536), gelu=True)
+        assert y.shape == pre.shape == (64, 1536)
+        clip = torch.empty(2, 3, 8, 224, 224)
+        col, geom = ops.stem_im2col(clip, torch.bfloat16)
+        assert col.shape == (2 * 8 * 112 * 112, 32) and geom == (16, 112, 112)
+        assert ops.patchify(clip).shape == (2, 8 * 28 * 28, 192)
