@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--resident", default="",
                     help="encoder stages kept resident in HBM (no checkpoint recompute): "
                          "comma list, or 'none'; default: the model's auto policy")
+    ap.add_argument("--lite", default="",
+                    help="encoder stages kept lite-resident (MBConv a1/a2 recomputed in the backward instead of "
+                         "the whole stage): comma list or 'none'; default: the model's auto policy")
     ap.add_argument("--probe", default="dec_attn_bwd",
                     help="kernel group timed with events for the roofline line: dec_attn_bwd (the top-time "
                          "kernels of the step: decoder attention dK/dV + dQ) or dec_attn_fwd")
@@ -152,6 +155,15 @@ def resident_used(model, frames, S):
         if r == "auto" else r
 
 
+def lite_used(model, frames, S):
+    from ssl_mae_amd.tiny_vit import auto_lite_stages
+    enc = model.encoder
+    if enc.lite_stages != "auto":
+        return list(enc.lite_stages)
+    return list(auto_lite_stages(frames, S, True, torch.device("cuda"), resident_used(model, frames, S),
+                                 key=(tuple(enc.depths), enc._sm_dec_depth)))
+
+
 def main():
     args = parse()
     from ssl_mae_amd import dist as smdist
@@ -186,6 +198,8 @@ def main():
     if args.resident:
         model.encoder.resident_stages = () if args.resident == "none" else \
             tuple(int(v) for v in args.resident.split(","))
+    if args.lite:
+        model.encoder.lite_stages = () if args.lite == "none" else tuple(int(v) for v in args.lite.split(","))
     torch.manual_seed(4321 + rank)               # per-rank mask stream
     opt = FusedAdamW(model.parameters(), lr=5e-4, weight_decay=0.05)
     scaler = GradScaler()
@@ -291,7 +305,8 @@ def main():
                        "global_batch": B * world,
                        "per_gpu_batch": B, "frames": T, "image_size": S, "mask_ratio": r,
                        "parallelism": f"dp{world}",
-                       "resident_stages": list(resident_used(model, B * T, S))},
+                       "resident_stages": list(resident_used(model, B * T, S)),
+                       "lite_stages": lite_used(model, B * T, S)},
             "roofline": roof,
             "model_tflops_per_gpu": round(step_tflops, 1) if step_tflops else None,
             "model_mfu": round(step_tflops / MFMA_BF16_PEAK_TFLOPS, 4) if step_tflops else None,

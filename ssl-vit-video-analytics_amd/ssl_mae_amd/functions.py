@@ -158,7 +158,11 @@ class MBConvFn(torch.autograd.Function):
     st.bn_updates: how many times the BatchNorm running statistics take this batch
     (2 reproduces a checkpointed stage's forward + recompute, TinyViT._run_stages);
     st.recompute_a1: drop the expand output a1 (the block's largest tensor) and
-    recompute its GEMM in the backward (bit-identical: same kernel, same inputs)."""
+    recompute its GEMM in the backward (bit-identical: same kernel, same inputs);
+    st.recompute_a2: also drop the depthwise output a2 and recompute it in the
+    backward from a1 with the saved BN0 statistics (no running-stat update) -- the
+    stage-0 "lite-resident" mode: two recomputed kernels instead of the whole
+    checkpointed stage forward."""
 
     @staticmethod
     def forward(ctx, x, st, w_exp, g0, b0, w_dw, g2, b2, w_fc0, w_fc2, w_proj, g5, b5):
@@ -199,8 +203,9 @@ class MBConvFn(torch.autograd.Function):
         ctx.st = st
         ctx.geom = (Fr, H, Wd, Cin, Ho, Wo)
         ctx.params = (w_exp, g0, b0, w_dw, g2, b2, w_fc0, w_fc2, w_proj, g5, b5)
-        ctx.save_for_backward(x, None if st.recompute_a1 else a1, a2, a3, m0, r0, m2, r2, m5, r5, pooled, h1se,
-                              gate)
+        lite = getattr(st, "recompute_a2", False)
+        ctx.save_for_backward(x, None if (st.recompute_a1 or lite) else a1, None if lite else a2, a3, m0, r0, m2, r2,
+                              m5, r5, pooled, h1se, gate)
         return out.view(Fr, Ho, Wo, Cout)
 
     @staticmethod
@@ -213,6 +218,14 @@ class MBConvFn(torch.autograd.Function):
         Fr, H, Wd, Cin, Ho, Wo = ctx.geom
         mid, Cout, s = st.mid, st.cout, st.stride
         _touch(*ctx.params)
+        if a2 is None:          # lite-resident: a1 and a2 recomputed from x (same kernels, saved stats)
+            a1 = K.linear(x.reshape(-1, Cin), W(w_exp, mode).view(mid, Cin))
+            if ctx.fused:
+                a2 = K.dwconv_fused(a1, (m0, r0, g0.detach(), b0.detach(), True), w_dw.detach().view(mid, 9), Fr,
+                                    H, Wd, mid, s)
+            else:
+                a2 = K.dwconv(K.bn_apply(a1, m0, r0, g0.detach(), b0.detach(), gelu=True),
+                              w_dw.detach().view(mid, 9), Fr, H, Wd, mid, s)
         dout2d = dout.reshape(-1, Cout).to(mode.act).contiguous()
         da3 = K.bn_bwd(dout2d, a3, m5, r5, g5.detach(), b5.detach(), False, G(g5), G(b5),
                        row_scale=st.dp_scale, rows_per_group=Ho * Wo)

@@ -86,7 +86,7 @@ class MBConv(nn.Module):
         dps = droppath_scale(self, x.shape[0], mode, 0, x.device) if self.use_res_connect else None
         st = _St(mode=mode, mid=self.mid, cout=self.out_chans, stride=self.stride, res=self.use_res_connect,
                  bn0=c[0].bn, bn2=c[2].bn, bn5=c[5].bn, dp_scale=dps, bn_updates=2 if resident else 1,
-                 recompute_a1=resident)
+                 recompute_a1=bool(resident), recompute_a2=resident == "lite")
         return MBConvFn.apply(x, st, c[0].c.weight, c[0].bn.weight, c[0].bn.bias, c[2].c.weight, c[2].bn.weight,
                               c[2].bn.bias, c[4].fc[0].weight, c[4].fc[2].weight, c[5].c.weight, c[5].bn.weight,
                               c[5].bn.bias)
@@ -178,6 +178,10 @@ class TinyViT(nn.Module):
         # recomputed under use_checkpoint (see _run_stages): a tuple, or "auto"
         # (auto_resident_stages: as many as the device memory holds).
         self.resident_stages = "auto"
+        # Stages kept "lite-resident": only block inputs / outputs and statistics are
+        # kept; the two largest tensors of each MBConv are recomputed in its backward
+        # instead of re-running the whole stage forward (stage 0: the 112x112 MBConvs).
+        self.lite_stages = "auto"
         self.embed_dims = list(embed_dims)
         self.depths = list(depths)
         self._sm_dec_depth = 4          # set by TinyVideoMAE (memory policy key)
@@ -218,15 +222,21 @@ class TinyViT(nn.Module):
         # non-reentrant checkpoint runs each stage's forward once and never recomputes
         # it, so BatchNorm takes the batch once: plain forward here too.
         grad = torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters()))
+        lite = self.lite_stages
+        key = (tuple(self.depths), self._sm_dec_depth)
         if resident == "auto":
-            resident = auto_resident_stages(x.shape[0], x.shape[1] * 2, mode.bf16, x.device,
-                                            key=(tuple(self.depths), self._sm_dec_depth)) \
+            resident = auto_resident_stages(x.shape[0], x.shape[1] * 2, mode.bf16, x.device, key=key) \
+                if self.use_checkpoint and self.training and grad else ()
+        if lite == "auto":
+            lite = auto_lite_stages(x.shape[0], x.shape[1] * 2, mode.bf16, x.device, resident, key=key) \
                 if self.use_checkpoint and self.training and grad else ()
         for i in range(n_stages):
             stage = self.stages[i]
             if self.use_checkpoint and self.training and grad:
                 if i in resident:
                     x = stage.run(x, mode, resident=True)
+                elif i in lite:
+                    x = stage.run(x, mode, resident="lite")
                 else:
                     x = checkpoint.checkpoint(stage.run, x, mode, use_reentrant=False)
             else:
@@ -286,6 +296,21 @@ def auto_resident_stages(frames, image_size, bf16, device, budget=0.85, key=((2,
         if policy in table and table[policy] * scale <= budget * total:
             return policy
     return ()
+
+
+# Extra peak per frame of keeping stage 0 lite-resident, on top of the resident policy
+# (GiB, measured like _PEAK_GIB_PER_FRAME); absent: not measured -> not used.
+_LITE0_EXTRA_GIB_PER_FRAME = {(((2, 2, 6, 2), 4), (1, 2)): 13.8 / 2048}   # 216.0 -> 229.8 GiB at B=256
+
+
+def auto_lite_stages(frames, image_size, bf16, device, resident, budget=0.92, key=((2, 2, 6, 2), 4)):
+    table = _PEAK_GIB_PER_FRAME.get(key)
+    extra = _LITE0_EXTRA_GIB_PER_FRAME.get((key, tuple(resident)))
+    if table is None or extra is None or tuple(resident) not in table:
+        return ()
+    total = torch.cuda.get_device_properties(device).total_memory / 2 ** 30
+    scale = frames * (image_size / 224.0) ** 2 * (1 if bf16 else 2)
+    return (0,) if (table[tuple(resident)] + extra) * scale <= budget * total else ()
 
 
 def index_modules(root):

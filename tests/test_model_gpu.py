@@ -72,17 +72,20 @@ def _run_steps(model, d, steps, bf16=False):
 GOLD = ["step_b2_t2_s32", "step_b2_t4_s64", "step_b1_t8_s224", "step_small_b2_t2_s32"]
 
 
-@pytest.mark.parametrize("resident", [(), (0, 1, 2)])
+@pytest.mark.parametrize("resident,lite", [((), ()), ((0, 1, 2), ()), ((1, 2), (0,))])
 @pytest.mark.parametrize("case", GOLD)
-def test_fp32_step_matches_reference_golden(golden_dir, case, resident):
-    """resident=(0, 1, 2): every stage kept in HBM (no checkpoint recompute) must give
-    the same loss, gradients, parameters and BN running stats (updated twice)."""
+def test_fp32_step_matches_reference_golden(golden_dir, case, resident, lite):
+    """resident=(0, 1, 2): every stage kept in HBM (no checkpoint recompute); lite=(0,):
+    stage 0 keeps only block inputs and recomputes a1/a2 in the backward.  Every policy
+    must give the same loss, gradients, parameters and BN running stats (updated twice
+    in stages 0-2, as the reference's checkpoint forward + recompute does)."""
     d = np.load(os.path.join(golden_dir, case + ".npz"))
     B, T, S = int(d["B"]), int(d["T"]), int(d["S"])
     small = "depths" in d.files and int(d["depths"][2]) == 12      # C3 "ViT-Small" (SURVEY.md H8)
     cfg = _cfg(B, T, S, float(d["ratio"]), int(d["decoder_depth"]) if "decoder_depth" in d.files else 4)
     model = _build(cfg, small)
     model.encoder.resident_stages = resident
+    model.encoder.lite_stages = lite
     # mask parity first (bit-exact): same seed, same RNG stream as the reference's step
     from ssl_mae_amd.mae_loader import get_tube_mask
     torch.manual_seed(42)
