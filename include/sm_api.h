@@ -121,6 +121,17 @@ int sm_conv_wpack(int out_dtype, const float* src, void* dst, int Cout, int Cin,
                   hipStream_t st);
 int sm_conv_wunpack_add(const float* packed, float* grad, int Cout, int Cin, int Kpad, int order,
                         hipStream_t st);
+/* Stem conv2 (tiny_vit.py:69, 3x3 / stride 1 / pad 1, bf16, channels-last) as GEMMs over
+ * the implicit im2col matrix -- no [pixels][9C] buffer in HBM.  wpack = sm_conv_wpack
+ * order 1 ([Cout][9*Cin]); wpack_t = order 2 ([Cin][9*Cout]); Cin, Cout % 8 == 0.
+ * fwd: y = conv(x); dgrad: dx = conv^T(dy); wgrad: dw[Cout][9*Cin] (+)= fp32 weight
+ * gradient (unpack with sm_conv_wunpack_add order 1). */
+int sm_conv3x3_fwd(const void* x, const void* wpack, void* y, int F, int H, int W, int Cin, int Cout, hipStream_t st);
+int sm_conv3x3_dgrad(const void* dy, const void* wpack_t, void* dx, int F, int H, int W, int Cin, int Cout,
+                     hipStream_t st);
+int64_t sm_conv3x3_wgrad_workspace_bytes(int F, int H, int W, int Cin, int Cout);
+int sm_conv3x3_wgrad(const void* dy, const void* x, float* dw, int accumulate, int F, int H, int W, int Cin, int Cout,
+                     void* ws, int64_t ws_bytes, hipStream_t st);
 int sm_dwconv_fwd(int dtype, const void* x, const float* w, void* y, int F, int H, int W, int C,
                   int stride, hipStream_t st);
 int64_t sm_dwconv_wgrad_workspace_bytes(int F, int H, int W, int C, int stride);

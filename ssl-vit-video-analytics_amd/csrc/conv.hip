@@ -112,17 +112,21 @@ __global__ void col2im3_kernel(const T* dcol, int F, int H, int W, int C, int Ho
 }
 
 // ------------------------------------------------------------------ weight pack
-// src [Cout][Cin][3][3] fp32 -> dst [Cout][Kpad]; order 0: k=(ci*9+ky*3+kx); 1: k=(ky*3+kx)*Cin+ci
+// src [Cout][Cin][3][3] fp32 -> order 0: dst[co][ci * 9 + tap]; order 1: dst[co][tap * Cin
+// + ci] (im2col3 / implicit conv3x3 forward); order 2: dst[ci][tap * Cout + co] (conv3x3
+// data gradient), tap = ky * 3 + kx; k >= 9 * (reduced channels) is zero padding.
 template <typename TO>
 __global__ void wpack_kernel(const float* src, TO* dst, int Cout, int Cin, int Kpad, int order) {
-  const int total = Cout * Kpad;
+  const int rows = order == 2 ? Cin : Cout;
+  const int total = rows * Kpad;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-    const int co = i / Kpad, k = i % Kpad;
+    const int row = i / Kpad, k = i % Kpad;
     float v = 0.f;
-    if (k < Cin * 9) {
-      int ci, tap;
-      if (order == 0) { ci = k / 9; tap = k % 9; }
-      else { tap = k / Cin; ci = k % Cin; }
+    if (k < (order == 2 ? Cout : Cin) * 9) {
+      int ci, co, tap;
+      if (order == 0) { co = row; ci = k / 9; tap = k % 9; }
+      else if (order == 1) { co = row; tap = k / Cin; ci = k % Cin; }
+      else { ci = row; tap = k / Cout; co = k % Cout; }
       v = src[(co * Cin + ci) * 9 + tap];
     }
     dst[i] = from_f<TO>(v);
@@ -961,7 +965,8 @@ extern "C" int sm_col2im3(int dtype, const void* dcol, int F, int H, int W, int 
 
 extern "C" int sm_conv_wpack(int out_dtype, const float* src, void* dst, int Cout, int Cin, int Kpad, int order,
                              hipStream_t st) {
-  const int total = Cout * Kpad;
+  if (order == 2 && Kpad < 9 * Cout) return -2;
+  const int total = (order == 2 ? Cin : Cout) * Kpad;
   DISPATCH1(out_dtype, hipLaunchKernelGGL(wpack_kernel<T>, dim3((total + 255) / 256), dim3(256), 0, st, src,
                                           (T*)dst, Cout, Cin, Kpad, order));
   SM_CHECK_LAUNCH();

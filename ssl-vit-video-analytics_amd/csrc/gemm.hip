@@ -41,6 +41,11 @@ struct GemmArgs {
   int64_t rows_per_group;
   float* partial;   // split-K fp32 slabs [z][M][N] (when non-null: raw store, no epilogue)
   float* colsum;    // bf16 v2, M/N-contiguous A only: per-split row sums of A, [z][M]
+  // implicit 3x3 / stride-1 / pad-1 convolution operand (conv3x3_* entry points): the
+  // operand is the im2col view of a channels-last [F][cH][cW][cC] tensor, k or n =
+  // tap * cC + c with tap = ky * 3 + kx, source pixel = pixel + (ky-1, kx-1), or
+  // + (1-ky, 1-kx) when cflip (data gradient).  Pixels outside the frame read zero.
+  int cH, cW, cC, cflip;
 };
 
 template <typename TC>
@@ -485,7 +490,119 @@ SM_DEV bf16x8 lread_frag_r(const char* lds, int rb, int s) {
   }
 }
 
-template <bool AK, bool BK, typename TC, bool VEC, int BMV>
+// ------------------------------------------------------------ implicit im2col loaders
+// The stem's 3x3 convolution (tiny_vit.py:69, 48 -> 96 channels at 112x112) as a GEMM
+// over the never-materialised im2col matrix (the 9x-inflated [pixels][9C] buffer the
+// explicit path writes and reads back): each 16-B chunk of a tile is 8 consecutive
+// channels of ONE source pixel (C % 8 == 0), so a chunk is still one buffer load, at
+// an offset computed per K-step from the chunk's tap and the row pixel's (y, x).
+// ConvRowsA: A(m, k) with m = output pixel (forward / data gradient), K-major tile.
+template <int ROWS, int NT>
+struct ConvRowsA {
+  static constexpr int CH = ROWS * 64 * 2 / 16 / NT;
+  int yx[CH];            // (y << 16) | x of row m, -1 past M
+  uint32_t roff[CH];     // bytes of row m's pixel relative to the block base (m0 - W - 1)
+  int loff0, kcur, tap, c;
+  SM_DEV void init(const GemmArgs& g, int m0, int kbeg) {
+    const int t = threadIdx.x, row = t >> 3, ch = t & 7;
+    loff0 = kmaj_off(row, ch);
+    const int HW = g.cH * g.cW;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int r = row + (NT / 8) * i;
+      const int m = m0 + r;
+      if (m < g.M) {
+        const int rem = m % HW;
+        yx[i] = ((rem / g.cW) << 16) | (rem % g.cW);
+      } else {
+        yx[i] = -1;
+      }
+      roff[i] = (uint32_t)((r + g.cW + 1) * g.cC) * 2u;
+    }
+    kcur = kbeg + ch * 8;
+    tap = kcur / g.cC;
+    c = kcur - tap * g.cC;
+  }
+  SM_DEV void load(__amdgpu_buffer_rsrc_t rs, const GemmArgs& g, int kend, uint4 (&r)[CH]) {
+    const int ky = (tap * 11) >> 5, kx = tap - 3 * ky;      // tap / 3, tap % 3 for tap < 9
+    const int oy = g.cflip ? 1 - ky : ky - 1, ox = g.cflip ? 1 - kx : kx - 1;
+    const bool kok = kcur < kend && tap < 9;
+    const int delta = ((oy * g.cW + ox) * g.cC + c) * 2;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int y = yx[i] >> 16, x = yx[i] & 0xFFFF;
+      const bool ok = kok && yx[i] >= 0 && (unsigned)(y + oy) < (unsigned)g.cH && (unsigned)(x + ox) < (unsigned)g.cW;
+      const uint32_t o = ok ? (uint32_t)((int)roff[i] + delta) : BUF_OOB;
+      r[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0));
+    }
+    kcur += BKT;
+    c += BKT;
+    while (c >= g.cC) {
+      c -= g.cC;
+      ++tap;
+    }
+  }
+  SM_DEV void store(char* lds, const uint4 (&r)[CH]) const {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) *(uint4*)(lds + loff0 + i * (NT / 8) * 128) = r[i];
+  }
+};
+
+// ConvColsB: B(k, n) with k = pixel (the reduction axis of the weight gradient) and
+// n = (tap, c), M/N-major tile: a thread's column chunk (tap, c) is fixed, its rows'
+// pixels advance by BKT per K-step (y, x kept incrementally).
+template <int ROWS, int NT>
+struct ConvColsB {
+  static constexpr int CH = ROWS * 64 * 2 / 16 / NT;
+  static constexpr int KSTEP = NT / (ROWS / 8);
+  int yx[CH];            // (y << 16) | x of pixel k0 + kk0 + KSTEP * i
+  int loff0, kk0, oy, ox;
+  uint32_t coff;         // bytes of (tap offset + c) relative to the row pixel at the step base
+  bool nok;
+  SM_DEV void init(const GemmArgs& g, int n0, int kbeg) {
+    const int t = threadIdx.x;
+    kk0 = t / (ROWS / 8);
+    const int col = (t % (ROWS / 8)) * 8;
+    loff0 = mnmaj_off_r<ROWS>(kk0, col);
+    const int n = n0 + col;
+    nok = n < g.N;
+    const int tap = n / g.cC, c = n - tap * g.cC;
+    const int ky = (tap * 11) >> 5, kx = tap - 3 * ky;
+    oy = ky - 1;
+    ox = kx - 1;
+    coff = (uint32_t)(((oy + 1) * g.cW + (ox + 1)) * g.cC + c) * 2u;
+    const int HW = g.cH * g.cW;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int rem = (kbeg + kk0 + KSTEP * i) % HW;
+      yx[i] = ((rem / g.cW) << 16) | (rem % g.cW);
+    }
+  }
+  SM_DEV void load(__amdgpu_buffer_rsrc_t rs, const GemmArgs& g, int kvalid, uint4 (&r)[CH]) {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int k = kk0 + KSTEP * i;
+      int y = yx[i] >> 16, x = yx[i] & 0xFFFF;
+      const bool ok = nok && k < kvalid && (unsigned)(y + oy) < (unsigned)g.cH && (unsigned)(x + ox) < (unsigned)g.cW;
+      const uint32_t o = ok ? (uint32_t)(k * g.cC * 2) + coff : BUF_OOB;
+      r[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0));
+      x += BKT;                       // next K-step: BKT pixels further
+      while (x >= g.cW) {
+        x -= g.cW;
+        if (++y == g.cH) y = 0;
+      }
+      yx[i] = (y << 16) | x;
+    }
+  }
+  SM_DEV void store(char* lds, const uint4 (&r)[CH]) const {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) *(uint4*)(lds + loff0 + i * KSTEP * ROWS * 2) = r[i];
+  }
+};
+
+// IMP: 0 plain operands; 1 A is the implicit im2col of a conv (ConvRowsA);
+// 2 B is (ConvColsB).
+template <bool AK, bool BK, typename TC, bool VEC, int BMV, int IMP = 0>
 __global__ __launch_bounds__(BMV * 2, BMV == 256 ? 4 : 2) void gemm_bf16_v2(GemmArgs g) {
   constexpr int NT = BMV * 2, BNV = 128;
   constexpr int LDS_MAIN = (BMV + BNV) * BKT * 2, LDS_EPI = (NT / 64) * 8192;   // operand tiles | row stage
@@ -507,12 +624,27 @@ __global__ __launch_bounds__(BMV * 2, BMV == 256 ? 4 : 2) void gemm_bf16_v2(Gemm
 
   TileLoader<BMV, NT, AK> tla;
   TileLoader<BNV, NT, BK> tlb;
-  tla.init(g.lda, g.M - m0);
-  tlb.init(g.ldb, g.N - n0);
+  ConvRowsA<BMV, NT> cla;
+  ConvColsB<BNV, NT> clb;
+  if constexpr (IMP == 1) cla.init(g, m0, kb);
+  else tla.init(g.lda, g.M - m0);
+  if constexpr (IMP == 2) clb.init(g, n0, kb);
+  else tlb.init(g.ldb, g.N - n0);
   // element offset of K-step k0 of each panel
   const int64_t abase = AK ? (int64_t)m0 * g.lda : (int64_t)m0;
   const int64_t bbase = BK ? (int64_t)n0 * g.ldb : (int64_t)n0;
   const int64_t astep = AK ? 1 : g.lda, bstep = BK ? 1 : g.ldb;
+  // implicit operands: A's descriptor sits at the block's first row pixel minus the
+  // (W + 1)-pixel halo; B's advances with K (its rows are pixels)
+  const int64_t cbase = -(int64_t)(g.cW + 1) * g.cC;
+  auto load_a = [&](int k0, uint4 (&r)[TileLoader<BMV, NT, AK>::CH]) {
+    if constexpr (IMP == 1) cla.load(panel_rsrc(A, (int64_t)m0 * g.cC + cbase), g, ke, r);
+    else tla.load(panel_rsrc(A, abase + k0 * astep), ke - k0, r);
+  };
+  auto load_b = [&](int k0, uint4 (&r)[TileLoader<BNV, NT, BK>::CH]) {
+    if constexpr (IMP == 2) clb.load(panel_rsrc(B, (int64_t)k0 * g.cC + cbase), g, ke - k0, r);
+    else tlb.load(panel_rsrc(B, bbase + k0 * bstep), ke - k0, r);
+  };
 
   f32x16 acc[2][2];
 #pragma unroll
@@ -524,8 +656,8 @@ __global__ __launch_bounds__(BMV * 2, BMV == 256 ? 4 : 2) void gemm_bf16_v2(Gemm
 
   uint4 ra[TileLoader<BMV, NT, AK>::CH], rb[TileLoader<BNV, NT, BK>::CH];
   if (kb < ke) {
-    tla.load(panel_rsrc(A, abase + kb * astep), ke - kb, ra);
-    tlb.load(panel_rsrc(B, bbase + kb * bstep), ke - kb, rb);
+    load_a(kb, ra);
+    load_b(kb, rb);
   }
   // Bias gradient of a weight-gradient GEMM (A = dy^T, M/N-contiguous): the n0 == 0
   // block of each m-tile also sums its A chunks over K (8 rows of M per thread, from
@@ -543,12 +675,14 @@ __global__ __launch_bounds__(BMV * 2, BMV == 256 ? 4 : 2) void gemm_bf16_v2(Gemm
         for (int j = 0; j < 8; ++j) cs8[j] += (float)v[j];
       }
     }
-    tla.store(la, ra);
-    tlb.store(lb, rb);
+    if constexpr (IMP == 1) cla.store(la, ra);
+    else tla.store(la, ra);
+    if constexpr (IMP == 2) clb.store(lb, rb);
+    else tlb.store(lb, rb);
     __syncthreads();
     if (k0 + BKT < ke) {
-      tla.load(panel_rsrc(A, abase + (k0 + BKT) * astep), ke - k0 - BKT, ra);
-      tlb.load(panel_rsrc(B, bbase + (k0 + BKT) * bstep), ke - k0 - BKT, rb);
+      load_a(k0 + BKT, ra);
+      load_b(k0 + BKT, rb);
     }
 #pragma unroll
     for (int s = 0; s < BKT / 16; ++s) {
@@ -725,7 +859,93 @@ int launch_layout(int abt, int ct, GemmArgs g, int splits, hipStream_t st) {
   return 0;
 }
 
+// implicit-conv GEMMs (bf16 operands, N % 8 == 0): IMP 1 = A implicit (forward,
+// data gradient: A K-major, B = packed weights [N][K]); IMP 2 = B implicit (weight
+// gradient: A = dy stored [K][M], fp32 split-K slabs)
+template <int IMP, typename TC>
+void launch_conv(const GemmArgs& g, int splits, hipStream_t st) {
+  const int v = gemm_variant(g.M, g.N) == 2 ? 2 : 3;
+  const int bm = variant_bm(v);
+  dim3 grid(((g.N + 127) / 128) * ((g.M + bm - 1) / bm), 1, splits);
+  constexpr bool AK = IMP == 1, BK = IMP == 1;
+  if (v == 2) hipLaunchKernelGGL((gemm_bf16_v2<AK, BK, TC, true, 256, IMP>), grid, dim3(512), 0, st, g);
+  else hipLaunchKernelGGL((gemm_bf16_v2<AK, BK, TC, true, 128, IMP>), grid, dim3(256), 0, st, g);
+}
+
+GemmArgs conv_args(int M, int N, int K, const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc,
+                   int H, int W, int Cs, int flip) {
+  GemmArgs g{};
+  g.M = M; g.N = N; g.K = K; g.A = A; g.lda = lda; g.B = B; g.ldb = ldb; g.C = C; g.ldc = ldc;
+  g.alpha = 1.f; g.beta = 0.f; g.rows_per_group = 1; g.k_begin = 0; g.k_chunk = K;
+  g.cH = H; g.cW = W; g.cC = Cs; g.cflip = flip;
+  return g;
+}
+
+bool conv_shape_ok(int64_t P, int H, int W, int Cin, int Cout, const void* a, const void* b, const void* c) {
+  return P > 0 && P < (1LL << 31) && H > 0 && W > 0 && W < 0x8000 && H < 0x8000 && Cin % 8 == 0 &&
+         Cout % 8 == 0 && ((((uintptr_t)a) | ((uintptr_t)b) | ((uintptr_t)c)) & 15) == 0;
+}
+
 }  // namespace
+
+// ---- stem conv2 (tiny_vit.py:69: 3x3, stride 1, pad 1) as implicit-im2col GEMMs ----
+// forward: y[p][co] = sum_{tap, ci} x[p + off(tap)][ci] * wpack[co][tap * Cin + ci]
+extern "C" int sm_conv3x3_fwd(const void* x, const void* wpack, void* y, int F, int H, int W, int Cin, int Cout,
+                              hipStream_t st) {
+  const int64_t P = (int64_t)F * H * W;
+  if (!conv_shape_ok(P, H, W, Cin, Cout, x, wpack, y)) return -2;
+  GemmArgs g = conv_args((int)P, Cout, 9 * Cin, x, Cin, wpack, 9 * Cin, y, Cout, H, W, Cin, 0);
+  launch_conv<1, __bf16>(g, 1, st);
+  SM_CHECK_LAUNCH();
+  return 0;
+}
+
+// data gradient: dx[p][ci] = sum_{tap, co} dy[p + (1-ky, 1-kx)][co] * wpack_t[ci][tap * Cout + co]
+extern "C" int sm_conv3x3_dgrad(const void* dy, const void* wpack_t, void* dx, int F, int H, int W, int Cin, int Cout,
+                                hipStream_t st) {
+  const int64_t P = (int64_t)F * H * W;
+  if (!conv_shape_ok(P, H, W, Cin, Cout, dy, wpack_t, dx)) return -2;
+  GemmArgs g = conv_args((int)P, Cin, 9 * Cout, dy, Cout, wpack_t, 9 * Cout, dx, Cin, H, W, Cout, 1);
+  launch_conv<1, __bf16>(g, 1, st);
+  SM_CHECK_LAUNCH();
+  return 0;
+}
+
+// weight gradient: dw[co][tap * Cin + ci] (+)= sum_p dy[p][co] * x[p + off(tap)][ci]  (fp32,
+// split-K over the pixels with a fixed-order slab reduction)
+extern "C" int64_t sm_conv3x3_wgrad_workspace_bytes(int F, int H, int W, int Cin, int Cout) {
+  const int64_t P = (int64_t)F * H * W;
+  const int s = choose_splits(Cout, 9 * Cin, (int)(P < (1LL << 31) ? P : (1LL << 31) - 1), true);
+  return s > 1 ? (int64_t)s * Cout * 9 * Cin * 4 : 0;
+}
+
+extern "C" int sm_conv3x3_wgrad(const void* dy, const void* x, float* dw, int accumulate, int F, int H, int W, int Cin,
+                                int Cout, void* ws, int64_t ws_bytes, hipStream_t st) {
+  const int64_t P = (int64_t)F * H * W;
+  if (!conv_shape_ok(P, H, W, Cin, Cout, dy, x, dw)) return -2;
+  const int N = 9 * Cin;
+  GemmArgs g = conv_args(Cout, N, (int)P, dy, Cout, x, N, dw, N, H, W, Cin, 0);
+  g.beta = accumulate ? 1.f : 0.f;
+  int splits = choose_splits(Cout, N, (int)P, true);
+  if (splits > 1 && (ws == nullptr || ws_bytes < (int64_t)splits * Cout * N * 4)) splits = 1;
+  if (splits > 1) {
+    int chunk = (int)((P + splits - 1) / splits);
+    chunk = (chunk + BKT - 1) / BKT * BKT;
+    splits = (int)((P + chunk - 1) / chunk);
+    g.k_chunk = chunk;
+    g.partial = (float*)ws;
+  }
+  launch_conv<2, float>(g, splits, st);
+  SM_CHECK_LAUNCH();
+  if (splits > 1) {
+    const int64_t total = (int64_t)Cout * N;
+    int blocks = (int)((total + 255) / 256);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(splitk_reduce_kernel<float>, dim3(blocks), dim3(256), 0, st, g, splits);
+    SM_CHECK_LAUNCH();
+  }
+  return 0;
+}
 
 extern "C" int64_t sm_gemm_workspace_bytes(int ab_dtype, int M, int N, int K) {
   const int s = choose_splits(M, N, K, ab_dtype == SM_BF16);

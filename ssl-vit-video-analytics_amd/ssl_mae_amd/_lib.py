@@ -58,6 +58,10 @@ _SIGS = {
     "sm_im2col3": (_c_i32, [_c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p]),
     "sm_col2im3": (_c_i32, [_c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p]),
     "sm_conv_wpack": (_c_i32, [_c_i32, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p]),
+    "sm_conv3x3_fwd": (_c_i32, [_c_p, _c_p, _c_p] + [_c_i32] * 5 + [_c_p]),
+    "sm_conv3x3_dgrad": (_c_i32, [_c_p, _c_p, _c_p] + [_c_i32] * 5 + [_c_p]),
+    "sm_conv3x3_wgrad_workspace_bytes": (_c_i64, [_c_i32] * 5),
+    "sm_conv3x3_wgrad": (_c_i32, [_c_p, _c_p, _c_p] + [_c_i32] * 6 + [_c_p, _c_i64, _c_p]),
     "sm_conv_wunpack_add": (_c_i32, [_c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p]),
     "sm_se_workspace_bytes": (_c_i64, [_c_i32, _c_i32, _c_i32]),
     "sm_se_fwd": (_c_i32, [_c_i32, _c_p] + [_c_p] * 4 + [_c_i32] * 5 + [_c_p] * 7 + [_c_i64, _c_p]),

@@ -107,11 +107,14 @@ class StemFn(torch.autograd.Function):
         a1 = K.linear(col1, w1p)
         del col1
         h1, m1, r1 = _bn_forward(a1, st.bn1, gelu=True)
-        col2 = K.im2col3(h1, Fr, Ho, Wo, 48, 1)
-        del h1
         w2p = K.conv_wpack(w2.detach(), 432, 1, act)
-        a2 = K.linear(col2, w2p)
-        del col2
+        if mode.bf16:       # conv2 as a GEMM over the implicit im2col of h1 (no 9x buffer)
+            a2 = K.conv3x3_fwd(h1, w2p, Fr, Ho, Wo, 48, 96)
+        else:               # fp32 parity path: explicit im2col + exact-fp32 GEMM
+            col2 = K.im2col3(h1, Fr, Ho, Wo, 48, 1)
+            a2 = K.linear(col2, w2p)
+            del col2
+        del h1
         y, m2, r2 = _bn_forward(a2, st.bn2, gelu=False)
         ctx.st = st
         ctx.geom = (Fr, Ho, Wo)
@@ -131,16 +134,22 @@ class StemFn(torch.autograd.Function):
         da2 = K.bn_bwd(dy, a2, m2, r2, g2.detach(), b2.detach(), False, G(g2), G(b2))
         del dy
         h1 = K.bn_apply(a1, m1, r1, g1.detach(), b1.detach(), gelu=True)
-        col2 = K.im2col3(h1, Fr, Ho, Wo, 48, 1)
-        del h1
         dw2p = torch.empty((96, 432), dtype=torch.float32, device=a1.device)
-        K.linear_dw(da2, col2, dw2p, accumulate=False)
-        del col2
+        if ctx.st.mode.bf16:     # implicit-im2col weight and data gradients
+            K.conv3x3_wgrad(da2, h1, dw2p, Fr, Ho, Wo, 48, 96, accumulate=False)
+            del h1
+            dh1 = K.conv3x3_dgrad(da2, K.conv_wpack(w2.detach(), 864, 2, act), Fr, Ho, Wo, 48, 96)
+            del da2
+        else:
+            col2 = K.im2col3(h1, Fr, Ho, Wo, 48, 1)
+            del h1
+            K.linear_dw(da2, col2, dw2p, accumulate=False)
+            del col2
+            dcol2 = K.linear_dx(da2, w2p)
+            del da2
+            dh1 = K.col2im3(dcol2, Fr, Ho, Wo, 48, 1)
+            del dcol2
         K.conv_wunpack_add(dw2p, G(w2), 1)
-        dcol2 = K.linear_dx(da2, w2p)
-        del da2
-        dh1 = K.col2im3(dcol2, Fr, Ho, Wo, 48, 1)
-        del dcol2
         da1 = K.bn_bwd(dh1, a1, m1, r1, g1.detach(), b1.detach(), True, G(g1), G(b1))
         del dh1
         col1, _ = K.stem_im2col(clip, act)

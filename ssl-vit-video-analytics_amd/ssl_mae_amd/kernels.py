@@ -261,10 +261,51 @@ def col2im3(dcol, F, H, W, C, stride):
 
 
 def conv_wpack(w, Kpad, order, dtype):
+    """w [Cout][Cin][3][3] fp32 -> packed [Cout][Kpad] (order 0 / 1) or [Cin][Kpad] (order 2)."""
     Cout, Cin = w.shape[0], w.shape[1]
-    out = torch.empty((Cout, Kpad), dtype=dtype, device=w.device)
+    out = torch.empty((Cin if order == 2 else Cout, Kpad), dtype=dtype, device=w.device)
     call("sm_conv_wpack", dt(out), ptr(w), ptr(out), Cout, Cin, Kpad, order, stream())
     return out
+
+
+def _conv_chk(t, C):
+    if t.dtype != torch.bfloat16 or not t.is_contiguous() or t.shape[-1] != C:
+        raise _lib.KernelError(f"conv3x3 operands are contiguous bf16 channels-last [pixels][{C}]")
+
+
+def conv3x3_fwd(x, wpack, F, H, W, Cin, Cout):
+    """Stem conv2 (3x3, stride 1, pad 1) over channels-last bf16 x [F*H*W, Cin] with
+    order-1 packed weights [Cout][9*Cin]: implicit-im2col GEMM -> y [F*H*W, Cout] bf16."""
+    _chk(x, wpack)
+    _conv_chk(x, Cin)
+    _conv_chk(wpack, 9 * Cin)
+    y = torch.empty((F * H * W, Cout), dtype=torch.bfloat16, device=x.device)
+    call("sm_conv3x3_fwd", ptr(x), ptr(wpack), ptr(y), F, H, W, Cin, Cout, stream())
+    return y
+
+
+def conv3x3_dgrad(dy, wpack_t, F, H, W, Cin, Cout):
+    """dL/dx of conv3x3_fwd from dy [F*H*W, Cout] and order-2 packed weights [Cin][9*Cout]."""
+    _chk(dy, wpack_t)
+    _conv_chk(dy, Cout)
+    _conv_chk(wpack_t, 9 * Cout)
+    dx = torch.empty((F * H * W, Cin), dtype=torch.bfloat16, device=dy.device)
+    call("sm_conv3x3_dgrad", ptr(dy), ptr(wpack_t), ptr(dx), F, H, W, Cin, Cout, stream())
+    return dx
+
+
+def conv3x3_wgrad(dy, x, dw_sink, F, H, W, Cin, Cout, accumulate=True):
+    """dw_sink [Cout][9*Cin] fp32 (+)= weight gradient of conv3x3_fwd (order-1 layout)."""
+    _chk(dy, x, dw_sink)
+    _conv_chk(dy, Cout)
+    _conv_chk(x, Cin)
+    if dw_sink.dtype != torch.float32 or dw_sink.shape != (Cout, 9 * Cin) or not dw_sink.is_contiguous():
+        raise _lib.KernelError("conv3x3_wgrad sink is contiguous fp32 [Cout][9*Cin]")
+    nbytes = query("sm_conv3x3_wgrad_workspace_bytes", F, H, W, Cin, Cout)
+    ws = _ws(nbytes, dy.device)
+    call("sm_conv3x3_wgrad", ptr(dy), ptr(x), ptr(dw_sink), 1 if accumulate else 0, F, H, W, Cin, Cout, ptr(ws),
+         nbytes, stream())
+    return dw_sink
 
 
 def conv_wunpack_add(packed, grad, order):

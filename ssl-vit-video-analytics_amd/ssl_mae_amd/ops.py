@@ -495,7 +495,8 @@ def _conv_wpack(w, Kpad, order, dtype):
     return _K.conv_wpack(w, Kpad, order, dtype)
 
 
-_conv_wpack.register_fake(lambda w, Kpad, order, dtype: w.new_empty((w.shape[0], Kpad), dtype=dtype))
+_conv_wpack.register_fake(lambda w, Kpad, order, dtype: w.new_empty((w.shape[1] if order == 2 else w.shape[0], Kpad),
+                                                                    dtype=dtype))
 
 
 def conv_wpack(w, Kpad, order, dtype):
@@ -512,6 +513,44 @@ _conv_wunpack_add.register_fake(_none)
 
 def conv_wunpack_add(packed, grad, order):
     torch.ops.ssl_mae.conv_wunpack_add(packed, grad, order)
+
+
+@_op("conv3x3_fwd", "(Tensor x, Tensor wpack, int F, int H, int W, int Cin, int Cout) -> Tensor")
+def _conv3x3_fwd(x, wpack, F, H, W, Cin, Cout):
+    return _K.conv3x3_fwd(x, wpack, F, H, W, Cin, Cout)
+
+
+_conv3x3_fwd.register_fake(lambda x, w, F, H, W, Cin, Cout: x.new_empty((F * H * W, Cout)))
+
+
+def conv3x3_fwd(x, wpack, F, H, W, Cin, Cout):
+    return torch.ops.ssl_mae.conv3x3_fwd(x, wpack, F, H, W, Cin, Cout)
+
+
+@_op("conv3x3_dgrad", "(Tensor dy, Tensor wpack_t, int F, int H, int W, int Cin, int Cout) -> Tensor")
+def _conv3x3_dgrad(dy, wpack_t, F, H, W, Cin, Cout):
+    return _K.conv3x3_dgrad(dy, wpack_t, F, H, W, Cin, Cout)
+
+
+_conv3x3_dgrad.register_fake(lambda dy, w, F, H, W, Cin, Cout: dy.new_empty((F * H * W, Cin)))
+
+
+def conv3x3_dgrad(dy, wpack_t, F, H, W, Cin, Cout):
+    return torch.ops.ssl_mae.conv3x3_dgrad(dy, wpack_t, F, H, W, Cin, Cout)
+
+
+@_op("conv3x3_wgrad", "(Tensor dy, Tensor x, Tensor(a!) dw_sink, int F, int H, int W, int Cin, int Cout, "
+                      "bool accumulate) -> ()", ("dw_sink",))
+def _conv3x3_wgrad(dy, x, dw_sink, F, H, W, Cin, Cout, accumulate):
+    _K.conv3x3_wgrad(dy, x, dw_sink, F, H, W, Cin, Cout, accumulate)
+
+
+_conv3x3_wgrad.register_fake(_none)
+
+
+def conv3x3_wgrad(dy, x, dw_sink, F, H, W, Cin, Cout, accumulate=True):
+    torch.ops.ssl_mae.conv3x3_wgrad(dy, x, dw_sink, F, H, W, Cin, Cout, bool(accumulate))
+    return dw_sink
 
 
 @_op("dwconv", "(Tensor x, Tensor w, int F, int H, int W, int C, int stride) -> Tensor")

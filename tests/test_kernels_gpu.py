@@ -633,3 +633,29 @@ def test_segment_mean_fwd_bwd():
     dy = rnd(G, C, seed=161).to(DEV)
     dx = kk.segment_mean_bwd(dy, G, R, C, torch.bfloat16)
     assert rel_err(dx, (dy / R)[:, None, :].expand(G, R, C).reshape(G * R, C)) < 1e-2
+
+
+@pytest.mark.parametrize("Fn,H,W,Cin,Cout", [(3, 14, 12, 48, 96), (2, 9, 23, 16, 24), (1, 112, 112, 48, 96)])
+def test_conv3x3_implicit_gemm(Fn, H, W, Cin, Cout):
+    """Stem conv2 as GEMMs over the implicit im2col (sm_conv3x3_fwd / _dgrad / _wgrad)
+    against F.conv2d fp32 autograd from the same bf16 inputs; frame borders, ragged
+    row tiles and a pixel count that is not a tile multiple."""
+    kk = KK()
+    x = rnd(Fn, H, W, Cin, dtype=torch.bfloat16, seed=170)
+    w = rnd(Cout, Cin, 3, 3, seed=171) * 0.1
+    xr = x.float().permute(0, 3, 1, 2).contiguous().requires_grad_(True)
+    wr = w.bfloat16().float().clone().requires_grad_(True)
+    yr = F.conv2d(xr, wr, None, 1, 1)
+    dy = rnd(*yr.shape, seed=172).to(torch.bfloat16)
+    yr.backward(dy.float())
+    wd = w.to(DEV)
+    y = kk.conv3x3_fwd(x.to(DEV).reshape(-1, Cin), kk.conv_wpack(wd, 9 * Cin, 1, torch.bfloat16), Fn, H, W, Cin, Cout)
+    assert rel_err(y, yr.permute(0, 2, 3, 1).reshape(-1, Cout)) < 2e-2
+    dyd = dy.permute(0, 2, 3, 1).reshape(-1, Cout).contiguous().to(DEV)
+    dx = kk.conv3x3_dgrad(dyd, kk.conv_wpack(wd, 9 * Cout, 2, torch.bfloat16), Fn, H, W, Cin, Cout)
+    assert rel_err(dx, xr.grad.permute(0, 2, 3, 1).reshape(-1, Cin)) < 2e-2
+    dwp = torch.full((Cout, 9 * Cin), 0.5, device=DEV)
+    kk.conv3x3_wgrad(dyd, x.to(DEV).reshape(-1, Cin), dwp, Fn, H, W, Cin, Cout, accumulate=True)
+    g = torch.zeros(Cout, Cin, 3, 3, device=DEV)
+    kk.conv_wunpack_add(dwp - 0.5, g, 1)
+    assert rel_err(g, wr.grad) < 2e-2
