@@ -384,6 +384,12 @@ __global__ void attn_delta_kernel(AttnArgs a, int D) {
 // =============================================================== bf16 backward dK, dV
 // Keys on lanes (32 per wave, 128 per block); Q / dO tiles (64 rows) staged to LDS
 // with register prefetch and read both row-wise (S, dP) and transposed (dV, dK).
+// Software-pipelined form: per 64-row tile the wave's two 32-row halves u = 0, 1 run
+// as  S,dP(0)  S,dP(1) | softmax(0) | dV,dK(0) | softmax(1) | dV,dK(1)  so each
+// half's exp / dropout / dS VALU stream has the other half's MFMAs to hide under.
+// Row constants folded in: without dropout the dP accumulator starts at -Delta
+// (dS = P * acc); with it, log2(1/(1-p)) is folded into the LSE so the exp yields
+// P' = P/(1-p) directly (dV needs no final scale) and Delta is stored as Delta(1-p).
 template <int D, bool DROP>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(AttnArgs a) {
   constexpr int QT = 64;
@@ -431,18 +437,77 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(AttnArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) { dk[t][r] = 0.f; dv[t][r] = 0.f; }
   const float c = a.scale * LOG2E;
-  const float ks = DROP ? 1.f / (1.f - a.drop_p) : 1.f;
+  const float lkeep = DROP ? log2f(1.f - a.drop_p) : 0.f;   // log2 of 1/ks
+  const float dkeep = DROP ? 1.f - a.drop_p : -1.f;         // stored Delta factor
   const uint32_t dthr = attn_thr(a.drop_p);
-  const int kq = l & 3;                       // == key & 3: byte of the shared hash
-  // Dropout: the hash of (query row, this key's 4-key group) covers the whole DPP
-  // quad of keys.  Lane kq hashes query row 4g + kq of each 16-row group, then a
-  // quad byte transpose hands every lane its own key's byte of all four rows.
-  // dlb = hash input of row q0 + 32u + 8g + 4h + kq minus the wave-uniform
-  // (q0 + 32u + 8g) * AG.
+  const int kq = l & 3;
   const uint32_t dlb = seed32(a.seed) + ((uint32_t)((uint64_t)(n * a.H + hd) * a.L) + 4 * h + kq) * AG +
                        (uint32_t)(key >> 2) * AC;
   uint32_t sel1, sel2;
   quad_sel(kq, sel1, sel2);
+
+  // S = Q K^T and dP = dO V^T for query rows q0 + 32u .. +31 (keys on lanes)
+  auto sdp = [&](int u, f32x16& sa, f32x16& da) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sa[r] = 0.f;
+    if (DROP) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) da[r] = 0.f;
+    } else {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {   // -Delta of rows 32u + 8g + 4h + j
+        const float4 b4 = *(const float4*)&ldel[32 * u + 8 * g + 4 * h];
+        da[4 * g] = b4.x; da[4 * g + 1] = b4.y; da[4 * g + 2] = b4.z; da[4 * g + 3] = b4.w;
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < D / 16; ++s) {
+      sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_b128(lq, roff[s] + u * RB), kf[s], sa, 0, 0, 0);
+      da = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_b128(ldo, roff[s] + u * RB), vf[s], da, 0, 0, 0);
+    }
+  };
+  // P (dropped, x 1/(1-p)) and dS as bf16 B-operand fragments
+  auto softmax = [&](int q0, int u, const f32x16& sa, const f32x16& da, bf16x8 (&pf)[2], bf16x8 (&sf)[2]) {
+    f32x16 pv, dsv;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      uint32_t kb4 = 0;
+      if (DROP)
+        kb4 = keep_bytes(keep_flags(quad_transpose_bytes(mix24(dlb + (uint32_t)(q0 + 32 * u + 8 * g) * AG), sel1, sel2), dthr));
+      const float4 a4 = *(const float4*)&llse[32 * u + 8 * g + 4 * h];
+      const float lse4[4] = {a4.x, a4.y, a4.z, a4.w};
+      float del4[4] = {0.f, 0.f, 0.f, 0.f};
+      if (DROP) {
+        const float4 b4 = *(const float4*)&ldel[32 * u + 8 * g + 4 * h];
+        del4[0] = b4.x; del4[1] = b4.y; del4[2] = b4.z; del4[3] = b4.w;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = 4 * g + j;
+        const float p = __builtin_amdgcn_exp2f(fmaf(sa[r], c, -lse4[j]));
+        if (DROP) {
+          const float pk = keep_sel(p, kb4, j);
+          pv[r] = pk;
+          dsv[r] = fmaf(pk, da[r], -(p * del4[j]));
+        } else {
+          pv[r] = p;
+          dsv[r] = p * da[r];
+        }
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) { pf[s] = acc_to_frag(pv, s); sf[s] = acc_to_frag(dsv, s); }
+  };
+  auto dvdk = [&](int u, const bf16x8 (&pf)[2], const bf16x8 (&sf)[2]) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int t = 0; t < D / 32; ++t) {
+        const int ob = u * RB + s * (RB / 2);
+        dv[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr(ldo, tlo[t] + ob, thi[t] + ob), pf[s], dv[t], 0, 0, 0);
+        dk[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr(lq, tlo[t] + ob, thi[t] + ob), sf[s], dk[t], 0, 0, 0);
+      }
+  };
 
   uint4 rq[Stager<D, QT>::CH], rd[Stager<D, QT>::CH];
   sq.load(qb, a.L, rq);
@@ -453,59 +518,22 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(AttnArgs a) {
     sd.store(ldo, rd);
     if (threadIdx.x < QT) {
       const int qq = q0 + threadIdx.x;
-      llse[threadIdx.x] = qq < a.L ? lse[qq] * LOG2E : 1e30f;   // invalid rows -> P = 0
-      ldel[threadIdx.x] = qq < a.L ? del[qq] : 0.f;
+      llse[threadIdx.x] = qq < a.L ? fmaf(lse[qq], LOG2E, lkeep) : 1e30f;   // invalid rows -> P = 0
+      ldel[threadIdx.x] = qq < a.L ? del[qq] * dkeep : 0.f;
     }
     __syncthreads();
     if (q0 + QT < a.L) {
       sq.load(qb + (int64_t)(q0 + QT) * ldq, a.L - q0 - QT, rq);
       sd.load(dob + (int64_t)(q0 + QT) * C, a.L - q0 - QT, rd);
     }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      f32x16 sacc, dpacc;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) { sacc[r] = 0.f; dpacc[r] = 0.f; }
-#pragma unroll
-      for (int s = 0; s < D / 16; ++s) {
-        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_b128(lq, roff[s] + u * RB), kf[s], sacc, 0, 0, 0);
-        dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_b128(ldo, roff[s] + u * RB), vf[s], dpacc, 0, 0, 0);
-      }
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        uint32_t kb4 = 0;   // byte j: keep flag of (query row 4g + j, this key)
-        if (DROP)
-          kb4 = keep_bytes(keep_flags(quad_transpose_bytes(mix24(dlb + (uint32_t)(q0 + 32 * u + 8 * g) * AG), sel1, sel2), dthr));
-        const float4 a4 = *(const float4*)&llse[32 * u + 8 * g + 4 * h];
-        const float4 b4 = *(const float4*)&ldel[32 * u + 8 * g + 4 * h];
-        const float lse4[4] = {a4.x, a4.y, a4.z, a4.w};
-        const float del4[4] = {b4.x, b4.y, b4.z, b4.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int r = 4 * g + j;
-          const float p = __builtin_amdgcn_exp2f(fmaf(sacc[r], c, -lse4[j]));
-          const float dp = dpacc[r];
-          if (DROP) {
-            sacc[r] = keep_sel(p, kb4, j);                            // dropped P feeds dV (x ks at the end)
-            dpacc[r] = p * fmaf(keep_sel(dp, kb4, j), ks, -del4[j]);   // dS
-          } else {
-            sacc[r] = p;
-            dpacc[r] = p * (dp - del4[j]);
-          }
-        }
-      }
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8 pf = acc_to_frag(sacc, s);
-        const bf16x8 sf = acc_to_frag(dpacc, s);
-#pragma unroll
-        for (int t = 0; t < D / 32; ++t) {
-          const int ob = u * RB + s * (RB / 2);
-          dv[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr(ldo, tlo[t] + ob, thi[t] + ob), pf, dv[t], 0, 0, 0);
-          dk[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr(lq, tlo[t] + ob, thi[t] + ob), sf, dk[t], 0, 0, 0);
-        }
-      }
-    }
+    f32x16 s0, p0, s1, p1;
+    bf16x8 pf0[2], sf0[2], pf1[2], sf1[2];
+    sdp(0, s0, p0);
+    sdp(1, s1, p1);
+    softmax(q0, 0, s0, p0, pf0, sf0);
+    dvdk(0, pf0, sf0);
+    softmax(q0, 1, s1, p1, pf1, sf1);
+    dvdk(1, pf1, sf1);
   }
   if (key < a.L) {
     __bf16* out = (__bf16*)a.out + ((int64_t)n * a.L + key) * ldq + hd * D;
@@ -515,7 +543,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(AttnArgs a) {
       for (int g = 0; g < 4; ++g) {
         float vk[4], vv[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) { vk[i] = dk[t][4 * g + i] * a.scale; vv[i] = dv[t][4 * g + i] * ks; }
+        for (int i = 0; i < 4; ++i) { vk[i] = dk[t][4 * g + i] * a.scale; vv[i] = dv[t][4 * g + i]; }
         store4(out + C + 32 * t + 8 * g + 4 * h, vk);
         store4(out + 2 * C + 32 * t + 8 * g + 4 * h, vv);
       }
