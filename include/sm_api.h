@@ -149,6 +149,16 @@ int sm_dwconv_fused_bwd(int F, int H, int W, int C, int stride, const void* dy, 
                         const float* in_mean, const float* in_rstd, const float* in_w, const float* in_b,
                         int in_gelu, const float* w, void* dx, float* dw, void* ws, int64_t ws_bytes,
                         hipStream_t st);
+// Stride-1 depthwise conv + BatchNorm(+GELU) backward that never stores the depthwise
+// data gradient (one pass over dy forming dw, dz = g GELU' and the BN sums, one
+// streaming pass dz -> dx, dx doubling as the dz buffer): dx = dL/dx for y = dwconv3x3(GELU(BN(x))), dw += dL/dw,
+// dgamma / dbeta += the BatchNorm's (MBConv conv1 -> act -> conv2, tiny_vit.py:36-56;
+// replaces sm_dwconv_fused_bwd + sm_bn_bwd on that path).
+int64_t sm_dwconv_bn_bwd_workspace_bytes(int F, int H, int W, int C);
+int sm_dwconv_bn_bwd(int F, int H, int W, int C, const void* dy, const void* x, const float* bn_mean,
+                     const float* bn_rstd, const float* bn_w, const float* bn_b, int bn_gelu, const float* w,
+                     void* dx, float* dw, float* dgamma, float* dbeta, void* ws, int64_t ws_bytes,
+                     hipStream_t st);
 int sm_dwconv_bwd(int dtype, const void* dy, const void* x, const float* w, void* dx, float* dw, int F,
                   int H, int W, int C, int stride, void* ws, int64_t ws_bytes, hipStream_t st);
 

@@ -117,6 +117,9 @@ def mbconv(args):
     rep("dwconv_fused s1 no-act", timeit(lambda: K.dwconv_fused(a, None, w, Fn, H, W, C, 1), args.iters), 2)
     dw = torch.zeros(C, 9, device=dev)
     rep("dwconv_fused_bwd s1", timeit(lambda: K.dwconv_fused_bwd(y, a, act, w, dw, Fn, H, W, C, 1), args.iters), 4)
+    g0, b0 = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    rep("dwconv_bn_bwd s1 (2 passes)", timeit(lambda: K.dwconv_bn_bwd(y, a, act, w, dw, g0, b0, Fn, H, W, C),
+                                              args.iters), 5)
     rep("dwconv_fused s2", timeit(lambda: K.dwconv_fused(a, act, w, Fn, H, W, C, 2), args.iters), 1.25)
     w1 = torch.randn(C // 4, C, device=dev) * 0.1
     w2 = torch.randn(C, C // 4, device=dev) * 0.1

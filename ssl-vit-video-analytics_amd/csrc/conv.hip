@@ -291,8 +291,13 @@ struct DwRing {
   uint4 raw[DWF_KV];
   SM_DEV int slot(int iy) const { return (iy + 1 + NR) % NR; }
   // raw-load rows [iy_first, iy_first + nrows) (nrows * W * 4 <= 256 * DWF_KV)
+  // REMAT: t passes through an empty asm so the per-chunk index math is redone per
+  // band rather than hoisted out of the band loop into ~40 long-lived VGPRs (for a
+  // consumer that needs the registers)
+  template <bool REMAT = false>
   SM_DEV void load(int iy_first, int nrows) {
-    const int t = threadIdx.x;
+    int t = threadIdx.x;
+    if (REMAT) asm volatile("" : "+v"(t));
     const int nvec = nrows * W * 4;
 #pragma unroll
     for (int k = 0; k < DWF_KV; ++k) {
@@ -304,8 +309,10 @@ struct DwRing {
       if (v < nvec && iy >= 0 && iy < H) raw[k] = *(const uint4*)(x + ((f * H + iy) * W + xx) * C + cbase);
     }
   }
+  template <bool REMAT = false>
   SM_DEV void commit(char* lds, const Affine8& af, int iy_first, int nrows) const {
-    const int t = threadIdx.x;
+    int t = threadIdx.x;
+    if (REMAT) asm volatile("" : "+v"(t));
     const int nvec = nrows * W * 4;
 #pragma unroll
     for (int k = 0; k < DWF_KV; ++k) {
@@ -333,12 +340,13 @@ struct DwRing {
     }
   }
   // the first band's NR rows (from iy0 = -1), in two register batches
+  template <bool REMAT = false>
   SM_DEV void stage_first(char* lds, const Affine8& af) {
     const int first = (NR + 1) / 2;
-    load(-1, first);
-    commit(lds, af, -1, first);
-    load(-1 + first, NR - first);
-    commit(lds, af, -1 + first, NR - first);
+    load<REMAT>(-1, first);
+    commit<REMAT>(lds, af, -1, first);
+    load<REMAT>(-1 + first, NR - first);
+    commit<REMAT>(lds, af, -1 + first, NR - first);
     zero_borders(lds);
   }
 };
@@ -347,7 +355,7 @@ struct DwRing {
 // the bijective XCD remap (as the attention and GEMM kernels): the C/32 slices of a
 // frame -- 64-B pieces of the same 128-B lines of every pixel -- run back to back on
 // one XCD, so each line is fetched into (and written back from) one L2 once rather
-// than half-used by two XCDs.  remap = 0: plain order (A/B switch SM_DWF_REMAP=0).
+// than half-used by two XCDs.  remap = 0: plain order.
 struct DwfBlock {
   int cs;
   int64_t f;
@@ -552,6 +560,208 @@ __global__ __launch_bounds__(256, 2) void dwf_wgrad_kernel(const __bf16* dy, con
       part[(f * C + cs * DWF_CB + t) * 9 + tap] = a;
     }
     __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------ depthwise + BN + GELU backward
+// MBConv's  y = dwconv3x3(h), h = GELU(u), u = BN(x) with batch statistics of x
+// (tiny_vit.py:36-56: conv1 -> act -> conv2), stride 1.  The depthwise data gradient
+// g = dL/dh (the 3x3 convolution of dy with the taps rotated 180 degrees) is never
+// stored; one pass (dwb_kernel) streams dy through the DwRing (zero halo) and reads x
+// at the thread's own pixels only, and from ONE GELU evaluation per element forms
+//   h (the forward's stored-precision activation) -> dw[c][tap] partials,
+//   dz = g GELU'(u)  -> stored (bf16, into the dx buffer), and the BatchNorm-backward
+//                        partial sums of dz and dz xhat;
+// a streaming pass (dwb_dx_kernel) then turns dz into dx = w rstd (dz - mean(dz) -
+// xhat mean(dz xhat)) in place.  HBM: dy read once, x twice, dz written and read
+// once, dx written once; the unfused sequence (depthwise dgrad, depthwise
+// wgrad, bn_bwd reduce, bn_bwd dx) reads dy / g four times and x three times, writes
+// twice, and evaluates GELU three times per element.
+// Thread = 4 channels (c4 = t & 7) x DWB_PX = 7 consecutive pixels of one row; h, GELU
+// and xhat of its pixels stay live across the tap loop.  Columns past the row's right
+// border read the next ring row (or the zeroed pad after the last one): finite
+// values that only reach pixels past W, whose h and GELU' are zero.
+constexpr int DWB_PX = 7, DWB_PAD = 8 * 64;
+typedef __attribute__((ext_vector_type(2))) unsigned int v2u32_t;
+
+template <bool GELU>
+__global__ __launch_bounds__(256, 2) void dwb_kernel(const __bf16* dy, const __bf16* x, ChanAffine bn,
+                                                     const float* w, __bf16* dz, float* part_w, float* part_bn,
+                                                     int H, int W, int C, int remap) {
+  using R = DwRing<1>;
+  constexpr int TY = R::TY;
+  constexpr int PX = DWB_PX;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const DwfBlock blk(C / DWF_CB, remap);
+  const int cs = blk.cs;
+  const int64_t f = blk.f;
+  const int t = threadIdx.x;
+  R ring{dy, f, H, W, C, cs * DWF_CB + (t & 3) * 8, t & 3, (W + 2) * 64};
+  Affine8 raw;
+  raw.init(ChanAffine{nullptr, nullptr, nullptr, nullptr, 0}, 0);
+  const int c4 = t & 7;
+  const int c0 = cs * DWF_CB + c4 * 4;
+  char* pad = lds + R::NR * ring.pitch;
+  for (int i = t; i < DWB_PAD / 16; i += 256) *(uint4*)(pad + 16 * i) = make_uint4(0, 0, 0, 0);
+  // rotated taps: wl[tap][ch] = w[ch][8 - tap]
+  float* wl = (float*)(pad + DWB_PAD);
+  for (int i = t; i < 9 * DWF_CB; i += 256) {
+    const int tap = i / DWF_CB, ch = i % DWF_CB;
+    wl[i] = w[(int64_t)(cs * DWF_CB + ch) * 9 + 8 - tap];
+  }
+  // per-channel BN constants [4][32]: scale, shift (u = x sc + sh), mean, rstd
+  float* cl = wl + 9 * DWF_CB;
+  if (t < DWF_CB) {
+    const int c = cs * DWF_CB + t;
+    const float r = bn.rstd[c], scv = r * bn.w[c];
+    cl[t] = scv;
+    cl[DWF_CB + t] = bn.b[c] - bn.mean[c] * scv;
+    cl[2 * DWF_CB + t] = bn.mean[c];
+    cl[3 * DWF_CB + t] = r;
+  }
+  float dwa[9][4], sdz[4], sdzx[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    sdz[j] = sdzx[j] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) dwa[k][j] = 0.f;
+  }
+  const int nstrip = (W + PX - 1) / PX;
+  const int items = TY * nstrip;
+  const int nbands = (H + TY - 1) / TY;
+  ring.stage_first<true>(lds, raw);
+  for (int band = 0; band < nbands; ++band) {
+    const int y0 = band * TY;
+    if (band > 0) {
+      __syncthreads();
+      ring.commit<true>(lds, raw, y0 + 1, R::NEW);
+    }
+    __syncthreads();
+    if (band + 1 < nbands) ring.load<true>(y0 + TY + 1, R::NEW);
+#pragma unroll 1
+    for (int it = t >> 3; it < items; it += 32) {
+      const int ry = it / nstrip, strip = it - ry * nstrip;
+      const int yi = y0 + ry;
+      if (yi >= H) continue;
+      const int xi0 = strip * PX;
+      // this pixel row of x and dz as buffer views: pixels past W read 0 / drop stores
+      const int64_t row0 = (f * H + yi) * W;
+      const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)(x + row0 * C), (short)0, W * C * 2, 0x00020000);
+      const auto zr = __builtin_amdgcn_make_buffer_rsrc((void*)(dz + row0 * C), (short)0, W * C * 2, 0x00020000);
+      const uint32_t off0 = (uint32_t)(xi0 * C + c0) * 2u;
+      float h[PX][4], gg[PX][4], g[PX][4];
+      bf16x4 xs[PX];                     // x itself (xhat is formed after the tap loop)
+      {
+        float sc[4], sh[4];
+        load4(cl + c4 * 4, sc);
+        load4(cl + DWF_CB + c4 * 4, sh);
+#pragma unroll
+        for (int p = 0; p < PX; ++p)
+          xs[p] = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(xr, off0 + p * C * 2, 0, 0));
+#pragma unroll
+        for (int p = 0; p < PX; ++p) {
+          const bool ok = xi0 + p < W;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float u = fmaf((float)xs[p][j], sc[j], sh[j]);
+            float cdf = 1.f, pdf = 0.f;
+            if (GELU) cdf = gelu_phi_pair(u, &pdf);
+            h[p][j] = ok ? (float)(__bf16)(GELU ? u * cdf : u) : 0.f;
+            gg[p][j] = ok ? fmaf(u, pdf, cdf) : 0.f;
+            g[p][j] = 0.f;
+          }
+          __builtin_amdgcn_sched_barrier(0);   // bound the interleaved GELU chains (VGPR budget)
+        }
+      }
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        const char* rowp = lds + ring.slot(yi - 1 + ky) * ring.pitch + c4 * 8 + xi0 * 64;
+        float wr[3][4];
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) load4(wl + (ky * 3 + kx) * DWF_CB + c4 * 4, wr[kx]);
+#pragma unroll
+        for (int ci = 0; ci < PX + 2; ++ci) {    // LDS column xi0 + ci = dy x + 1
+          float v[4];
+          load4((const __bf16*)(rowp + ci * 64), v);
+#pragma unroll
+          for (int p = 0; p < PX; ++p) {
+            const int kx = ci - p;
+            if (kx < 0 || kx > 2) continue;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              g[p][j] = fmaf(v[j], wr[kx][j], g[p][j]);
+              dwa[8 - (ky * 3 + kx)][j] = fmaf(v[j], h[p][j], dwa[8 - (ky * 3 + kx)][j]);
+            }
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);   // one tap row's reads in flight at a time (VGPR budget)
+      }
+      float mu[4], rs[4];
+      load4(cl + 2 * DWF_CB + c4 * 4, mu);
+      load4(cl + 3 * DWF_CB + c4 * 4, rs);
+#pragma unroll
+      for (int p = 0; p < PX; ++p) {
+        float d[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          d[j] = (float)(__bf16)(g[p][j] * gg[p][j]);   // the stored dz: the sums see what dx will
+          sdz[j] += d[j];
+          sdzx[j] = fmaf(d[j], ((float)xs[p][j] - mu[j]) * rs[j], sdzx[j]);
+        }
+        bf16x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = (__bf16)d[j];
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, o), zr, off0 + p * C * 2, 0, 0);
+      }
+    }
+  }
+  __syncthreads();                     // ring dead: reuse for the reductions
+  float* red = (float*)lds;            // [256][4]
+  auto reduce = [&](const float* v4, float* dst, int64_t stride) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[t * 4 + j] = v4[j];
+    __syncthreads();
+    if (t < DWF_CB) {
+      const int cc = t >> 2, j = t & 3;
+      float s = 0.f;
+      for (int k = 0; k < 32; ++k) s += red[(k * 8 + cc) * 4 + j];
+      dst[(int64_t)t * stride] = s;
+    }
+    __syncthreads();
+  };
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) reduce(dwa[tap], part_w + (f * C + cs * DWF_CB) * 9 + tap, 9);
+  reduce(sdz, part_bn + (f * 2 + 0) * C + cs * DWF_CB, 1);
+  reduce(sdzx, part_bn + (f * 2 + 1) * C + cs * DWF_CB, 1);
+}
+
+// dx = w rstd (dz - coef[0] - xhat coef[1]) in place over dz; thread = fixed 8-channel
+// chunk (C / 8 <= 256) over a block's rows
+__global__ __launch_bounds__(256) void dwb_dx_kernel(const __bf16* x, ChanAffine bn, const float* coef, __bf16* dz,
+                                                     int64_t M, int C, int rows_per_block) {
+  const int nch = C / 8, rpp = 256 / nch;
+  const int chunk = threadIdx.x % nch, r = threadIdx.x / nch;
+  if (r >= rpp) return;
+  float mu[8], rs[8], wr[8], k0[8], k1[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = chunk * 8 + j;
+    mu[j] = bn.mean[c];
+    rs[j] = bn.rstd[c];
+    wr[j] = bn.w[c] * rs[j];
+    k0[j] = coef[c];
+    k1[j] = coef[C + c];
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
+  for (int64_t row = r0 + r; row < r1; row += rpp) {
+    const int64_t e = row * C + chunk * 8;
+    float xv[8], dv[8], o[8];
+    load8(x + e, xv);
+    load8(dz + e, dv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = wr[j] * (dv[j] - k0[j] - (xv[j] - mu[j]) * rs[j] * k1[j]);
+    store8(dz + e, o);
   }
 }
 
@@ -1007,10 +1217,7 @@ static size_t dwf_lds_bytes(int W, int stride) {
   return lds < 256 * 16 * 4 ? 256 * 16 * 4 : lds;   // the statistics reduction reuses it
 }
 
-static int dwf_remap() {
-  static const int r = [] { const char* e = getenv("SM_DWF_REMAP"); return e ? atoi(e) : 1; }();
-  return r;
-}
+static int dwf_remap() { return 1; }
 
 static bool dwf_shape_ok(int F, int W, int C, int stride) {
   return C % DWF_CB == 0 && (stride == 1 || stride == 2) && F > 0 && (int64_t)F * (C / DWF_CB) < (1LL << 31) &&
@@ -1083,6 +1290,45 @@ extern "C" int sm_dwconv_fused_bwd(int F, int H, int W, int C, int stride, const
     hipLaunchKernelGGL((dwf_wgrad_kernel<2>), g2, dim3(256), lds, st, (const __bf16*)dy, (const __bf16*)x, act, part,
                        H, W, C, Ho, Wo, dwf_remap());
   colred(part, F, C * 9, nullptr, dw, 1, st);
+  SM_CHECK_LAUNCH();
+  return 0;
+}
+
+// Stride-1 depthwise + BatchNorm(+GELU) backward (dwb_kernel): dx = dL/dx for
+// y = dwconv3x3(GELU(BN(x))), dw += dL/dw, dgamma / dbeta += the BatchNorm's.
+extern "C" int64_t sm_dwconv_bn_bwd_workspace_bytes(int F, int H, int W, int C) {
+  return ((int64_t)F * C * 9 + (int64_t)F * 2 * C + 2 * C) * 4 + 2 * C * 8 + 64;
+}
+
+extern "C" int sm_dwconv_bn_bwd(int F, int H, int W, int C, const void* dy, const void* x, const float* bn_mean,
+                                const float* bn_rstd, const float* bn_w, const float* bn_b, int bn_gelu,
+                                const float* w, void* dx, float* dw, float* dgamma, float* dbeta, void* ws,
+                                int64_t ws_bytes, hipStream_t st) {
+  if (!dwf_shape_ok(F, W, C, 1) || !bn_mean || !dx || dwf_lds_bytes(W, 1) + DWB_PAD + 4 * DWF_CB * 4 > 64 * 1024) return -2;
+  if (((uintptr_t)x & 15) || ((uintptr_t)dy & 15) || ((uintptr_t)dx & 15) || C / 8 > 256) return -2;
+  if (ws_bytes < sm_dwconv_bn_bwd_workspace_bytes(F, H, W, C)) return -4;
+  float* part_w = (float*)ws;
+  float* part_bn = part_w + (int64_t)F * C * 9;
+  float* coef = part_bn + (int64_t)F * 2 * C;
+  double* sums = (double*)(((uintptr_t)(coef + 2 * C) + 7) & ~(uintptr_t)7);
+  ChanAffine bn{bn_mean, bn_rstd, bn_w, bn_b, bn_gelu};
+  const dim3 grid((C / DWF_CB) * F);
+  const size_t lds = dwf_lds_bytes(W, 1) + DWB_PAD + 4 * DWF_CB * 4;
+  if (bn_gelu)
+    hipLaunchKernelGGL(dwb_kernel<true>, grid, dim3(256), lds, st, (const __bf16*)dy, (const __bf16*)x, bn, w,
+                       (__bf16*)dx, part_w, part_bn, H, W, C, dwf_remap());
+  else
+    hipLaunchKernelGGL(dwb_kernel<false>, grid, dim3(256), lds, st, (const __bf16*)dy, (const __bf16*)x, bn, w,
+                       (__bf16*)dx, part_w, part_bn, H, W, C, dwf_remap());
+  colred(part_w, F, C * 9, nullptr, dw, 1, st);
+  colred(part_bn, F, 2 * C, sums, nullptr, 0, st);
+  const int64_t M = (int64_t)F * H * W;
+  hipLaunchKernelGGL(se_bn_finalize_kernel, dim3((C + 127) / 128), dim3(128), 0, st, sums, M, C, dgamma, dbeta,
+                     coef);
+  int64_t rpb = (M + 4095) / 4096;
+  if (rpb < 16) rpb = 16;
+  hipLaunchKernelGGL(dwb_dx_kernel, dim3((unsigned)((M + rpb - 1) / rpb)), dim3(256), 0, st, (const __bf16*)x, bn,
+                     (const float*)coef, (__bf16*)dx, M, C, (int)rpb);
   SM_CHECK_LAUNCH();
   return 0;
 }

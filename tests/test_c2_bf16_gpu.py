@@ -199,7 +199,7 @@ class _BN:
         self.momentum, self.eps = 0.1, 1e-5
 
 
-@pytest.mark.parametrize("Fr,H,C,stride", [(16, 112, 384, 1), (16, 112, 384, 2), (16, 56, 768, 2)])
+@pytest.mark.parametrize("Fr,H,C,stride", [(16, 112, 384, 1), (16, 112, 384, 2), (16, 56, 768, 2), (4, 19, 64, 1)])
 def test_mbconv_fused_middle_vs_fp32_torch(Fr, H, C, stride):
     """BN0+GELU folded into the depthwise conv, BN2 statistics from its epilogue,
     BN2+GELU folded into SE (sm_dwconv_fused_fwd / sm_se_fwd), and the fused
@@ -267,6 +267,20 @@ def test_mbconv_fused_middle_vs_fp32_torch(Fr, H, C, stride):
     # reference's autocast backward: 3e-2, like da1
     for got, ref, nm in ((dg0, tg0.grad, "bn0.w"), (db0, tb0.grad, "bn0.b")):
         assert rel(got, ref) < 3e-2, nm
+    if stride == 1:
+        # the two-pass depthwise + BN0/GELU backward (sm_dwconv_bn_bwd) the stride-1
+        # MBConvs run: same references, and close to the unfused sequence above
+        dwdw_b = torch.zeros(C, 9, device=DEV)
+        dg0_b = torch.zeros(C, device=DEV)
+        db0_b = torch.zeros(C, device=DEV)
+        da1_b = kk.dwconv_bn_bwd(da2, a1, act0, wdw, dwdw_b, dg0_b, db0_b, Fr, H, W, C)
+        torch.cuda.synchronize()
+        assert rel(da1_b, xa.grad) < 3e-2
+        assert rel(da1_b, da1) < 2e-2
+        assert rel(dwdw_b, tw.grad) < 2e-2
+        assert rel(dwdw_b, dwdw) < 1e-2
+        for got, ref, nm in ((dg0_b, tg0.grad, "bn0.w"), (db0_b, tb0.grad, "bn0.b")):
+            assert rel(got, ref) < 3e-2, nm
 
 
 # ------------------------------------------------------------------ whole model, bf16
