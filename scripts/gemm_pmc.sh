@@ -1,6 +1,10 @@
-# PMC counters of the GEMM kernels on the bench shapes (kbench gemm), one pass per counter set
+set -e
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-ONLY=${1:-dec qkv}
-timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_WAIT_ANY -d gpurun_out/gpmc1 -o run --output-format csv -- python scripts/kbench.py gemm --iters 1 --only "$ONLY" > gpurun_out/gpmc1.log 2>&1 && \
-timeout -s KILL 120 rocprofv3 --pmc SQ_ACTIVE_INST_VMEM SQ_INST_LEVEL_VMEM SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_CYCLES -d gpurun_out/gpmc2 -o run --output-format csv -- python scripts/kbench.py gemm --iters 1 --only "$ONLY" > gpurun_out/gpmc2.log 2>&1 && \
-timeout -s KILL 120 rocprofv3 --pmc TA_BUSY_avr TA_BUSY_max TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum -d gpurun_out/gpmc3 -o run --output-format csv -- python scripts/kbench.py gemm --iters 1 --only "$ONLY" > gpurun_out/gpmc3.log 2>&1
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "gelu_backward_epilogue or dropout_masks or gemm" > gpurun_out/gemm_tests.log 2>&1
+A="scripts/kbench.py gemm --batch 32 --iters 1 --only s0"
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/gpmc_p3 -o run --output-format csv -- python $A > gpurun_out/gpmc_p3.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/gpmc_p4 -o run --output-format csv -- python $A > gpurun_out/gpmc_p4.log 2>&1
+bash scripts/pmc_kernel.sh gpmc scripts/kbench.py gemm --batch 32 --iters 1 --only "s0 expand"
+python scripts/pmc_sum.py gpurun_out/gpmc > gpurun_out/gpmc_sum.txt
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/gstat -o run -- python3 scripts/kbench.py gemm --batch 256 --iters 2 > gpurun_out/gemm_shapes.log 2>&1

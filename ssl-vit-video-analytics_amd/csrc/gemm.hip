@@ -32,8 +32,9 @@ struct GemmArgs {
   void* C; int64_t ldc;
   const float* bias;
   float alpha, beta;
-  int epi;          // bit0: exact GELU; bit1: round the branch to bf16 before the residual add
-  void* aux;        // pre-activation output (same dtype/ld as C) when GELU
+  int epi;          // bit0: exact GELU; bit1: round the branch to bf16 before the residual add;
+                    // bit2: GELU backward, C = acc * GELU'(aux) (aux = the saved pre-activation)
+  void* aux;        // pre-activation output (same dtype/ld as C) when GELU; input with bit2
   const void* R;    // residual input (dtype/ld of C); null with beta != 0 -> C itself
   float drop_p;     // dropout on the branch (before the residual add / after GELU)
   uint64_t seed;
@@ -59,6 +60,7 @@ SM_DEV void epilogue_store(const GemmArgs& g, int64_t row, int col, float acc) {
   TC* C = (TC*)g.C;
   const int64_t idx = row * g.ldc + col;
   if (g.epi & 2) v = (float)(__bf16)v;   // autocast: the Linear output is bf16 before the fp32 add
+  if (g.epi & 4) v *= gelu_grad(to_f<TC>(((const TC*)g.aux)[idx]));
   if (g.epi & 1) {
     if (g.aux) ((TC*)g.aux)[idx] = from_f<TC>(v);
     v = gelu_f(v);
@@ -300,6 +302,12 @@ SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x
           if (g.epi & 2) v[e] = (float)(__bf16)v[e];
         }
         const int64_t idx = row * g.ldc + col;
+        if (g.epi & 4) {   // GELU backward: the saved pre-activation run of this (row, cols)
+          float pre[8];
+          load8((const TC*)g.aux + idx, pre);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] *= gelu_grad(pre[e]);
+        }
         if (g.epi & 1) {
           if (g.aux) {
             if (stage) stage_put<TC>(rs_, 1, j, p, h, l, v);

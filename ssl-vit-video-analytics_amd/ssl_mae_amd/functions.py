@@ -337,10 +337,10 @@ class BlockFn(torch.autograd.Function):
         h = K.gelu(hpre, st.drop_ff, st.seed_ff)
         K.linear_dw_bias(db, h, G(w2), G(b2))
         del h
-        dh = K.linear_dx(db, W(w2, mode))
+        # dL/dhpre straight from the fc2 data-gradient GEMM's epilogue (keep mask and
+        # GELU' applied there: no dh round trip, no gelu_bwd pass)
+        dhpre = K.linear_dx(db, W(w2, mode), gelu_pre=hpre, drop_p=st.drop_ff, seed=st.seed_ff)
         del db
-        dhpre = K.gelu_bwd(hpre, dh, st.drop_ff, st.seed_ff)
-        del dh
         ln2 = K.layernorm(x2, ln2w.detach(), ln2b.detach(), out_dtype=act, eps=st.eps)[0]
         K.linear_dw_bias(dhpre, ln2, G(w1), G(b1))
         del ln2

@@ -24,14 +24,15 @@ def _ws(nbytes, device):
 
 # ------------------------------------------------------------------ GEMM
 def gemm(A, B, C, M, N, K, a_layout, b_layout, lda, ldb, ldc, bias=None, alpha=1.0, beta=0.0,
-         gelu=False, aux=None, R=None, round_branch=False, drop_p=0.0, seed=0, row_scale=None, rows_per_group=1):
+         gelu=False, aux=None, R=None, round_branch=False, drop_p=0.0, seed=0, row_scale=None, rows_per_group=1,
+         gelu_bwd=False):
     _chk(A, B, C)
     ab = dt(A)
     if dt(B) != ab:
         raise _lib.KernelError("GEMM operands must share a dtype")
     nbytes = query("sm_gemm_workspace_bytes", ab, M, N, K)
     ws = _ws(nbytes, A.device) if nbytes else None
-    epi = (1 if gelu else 0) | (2 if round_branch else 0)
+    epi = (1 if gelu else 0) | (2 if round_branch else 0) | (4 if gelu_bwd else 0)
     call("sm_gemm", ab, dt(C), a_layout, b_layout, M, N, K, ptr(A), lda, ptr(B), ldb, ptr(C), ldc, ptr(bias),
          float(alpha), float(beta), epi, ptr(aux), ptr(R), float(drop_p), int(seed) & ((1 << 64) - 1), ptr(row_scale),
          int(rows_per_group), ptr(ws), nbytes, stream())
@@ -51,11 +52,19 @@ def linear(x, w, bias=None, out_dtype=None, gelu=False, residual=None, round_bra
     return (out, pre) if gelu else out
 
 
-def linear_dx(dy, w, out_dtype=None, residual=None):
-    """dx = dy @ w (+ residual);  dy [M,N], w [N,K]."""
+def linear_dx(dy, w, out_dtype=None, residual=None, gelu_pre=None, drop_p=0.0, seed=0):
+    """dx = dy @ w (+ residual);  dy [M,N], w [N,K].  gelu_pre: the input of a GELU (with
+    dropout drop_p / seed on its output) that produced this Linear's input: returns the
+    gradient w.r.t. that pre-activation, dx * keep/(1-p) * GELU'(gelu_pre), in the
+    epilogue (no dh round trip, no separate gelu_bwd pass)."""
     M, N = dy.shape
     K = w.shape[1]
     out = torch.empty((M, K), dtype=out_dtype or dy.dtype, device=dy.device)
+    if gelu_pre is not None:
+        if gelu_pre.shape != out.shape or gelu_pre.dtype != out.dtype or residual is not None:
+            raise _lib.KernelError("linear_dx: gelu_pre must match dx's shape/dtype (no residual)")
+        gemm(dy, w, out, M, K, N, 0, 1, N, K, K, aux=gelu_pre.contiguous(), gelu_bwd=True, drop_p=drop_p, seed=seed)
+        return out
     gemm(dy, w, out, M, K, N, 0, 1, N, K, K, beta=1.0 if residual is not None else 0.0, R=residual)
     return out
 

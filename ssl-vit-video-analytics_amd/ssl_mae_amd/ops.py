@@ -123,18 +123,19 @@ def linear(x, w, bias=None, out_dtype=None, gelu=False, residual=None, round_bra
     return (y, pre) if gelu else y
 
 
-@_op("linear_dx", "(Tensor dy, Tensor w, ScalarType? out_dtype, Tensor? residual) -> Tensor")
-def _linear_dx(dy, w, out_dtype, residual):
-    return _K.linear_dx(dy, w, out_dtype, residual)
+@_op("linear_dx", "(Tensor dy, Tensor w, ScalarType? out_dtype, Tensor? residual, Tensor? gelu_pre, float drop_p, "
+                  "int seed) -> Tensor")
+def _linear_dx(dy, w, out_dtype, residual, gelu_pre, drop_p, seed):
+    return _K.linear_dx(dy, w, out_dtype, residual, gelu_pre, drop_p, _u64(seed))
 
 
 @_linear_dx.register_fake
-def _(dy, w, out_dtype, residual):
+def _(dy, w, out_dtype, residual, gelu_pre, drop_p, seed):
     return dy.new_empty((dy.shape[0], w.shape[1]), dtype=out_dtype or dy.dtype)
 
 
-def linear_dx(dy, w, out_dtype=None, residual=None):
-    return torch.ops.ssl_mae.linear_dx(dy, w, out_dtype, residual)
+def linear_dx(dy, w, out_dtype=None, residual=None, gelu_pre=None, drop_p=0.0, seed=0):
+    return torch.ops.ssl_mae.linear_dx(dy, w, out_dtype, residual, gelu_pre, float(drop_p), _s64(seed))
 
 
 @_op("linear_dw", "(Tensor dy, Tensor x, Tensor(a!) grad_sink, bool accumulate) -> ()", ("grad_sink",))

@@ -579,6 +579,27 @@ def test_dropout_masks_fwd_bwd_consistent():
     assert abs((s > 0).float().mean() - 0.9) < 0.02
 
 
+@pytest.mark.parametrize("dtype,p", [(torch.bfloat16, 0.1), (torch.bfloat16, 0.0), (torch.float32, 0.1)])
+def test_linear_dx_gelu_backward_epilogue(dtype, p):
+    """fc2's data gradient with GELU' and the fc1 output's dropout mask applied in the
+    GEMM epilogue (BlockFn backward) == linear_dx followed by gelu_bwd, and == the fp32
+    torch autograd of dropout(GELU(pre)) @ w^T."""
+    kk = KK()
+    M, N, Kd, seed = 777, 384, 1536, 4321
+    dy = rnd(M, N, dtype=dtype, seed=150).to(DEV)
+    w = rnd(N, Kd, dtype=dtype, seed=151, scale=0.05).to(DEV)
+    pre = rnd(M, Kd, dtype=dtype, seed=152).to(DEV)
+    got = kk.linear_dx(dy, w, gelu_pre=pre, drop_p=p, seed=seed)
+    ref2 = kk.gelu_bwd(pre, kk.linear_dx(dy, w), p, seed)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert rel_err(got, ref2) < tol
+    keep = (kk.gelu(pre, p, seed).float() != 0) | (kk.gelu(pre).float() == 0)
+    pr = pre.float().requires_grad_(True)
+    h = F.gelu(pr) * keep / (1 - p)
+    h.backward(dy.float() @ w.float())
+    assert rel_err(got, pr.grad) < tol
+
+
 @pytest.mark.parametrize("M", [98, 49, 1001])
 def test_weight_grad_any_row_count(M):
     """dW = dy^T x over a token-row count that is not a multiple of 8 (fine-tune
