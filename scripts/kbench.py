@@ -72,6 +72,28 @@ def gemm(args):
         torch.cuda.empty_cache()
 
 
+def dw(args):
+    """Every weight-gradient GEMM shape of the step: dW[nout][nin] = dy^T x (+ db)."""
+    B = args.batch
+    cases = [("dec/s2 fc2", B * 6272, 384, 1536), ("dec/s2 fc1", B * 6272, 1536, 384),
+             ("dec/s2 qkv", B * 6272, 1152, 384), ("dec/s2 proj", B * 6272, 384, 384),
+             ("s1 fc1", B * 8 * 3136, 768, 192), ("s1 fc2", B * 8 * 3136, 192, 768),
+             ("s1 qkv", B * 8 * 3136, 576, 192), ("s1 proj", B * 8 * 3136, 192, 192),
+             ("s0 expand", B * 8 * 12544, 384, 96), ("s0 proj", B * 8 * 12544, 96, 384)]
+    for name, M, nout, nin in cases:
+        if args.only and args.only not in name:
+            continue
+        dy = torch.randn(M, nout, device="cuda").to(torch.bfloat16)
+        x = torch.randn(M, nin, device="cuda").to(torch.bfloat16)
+        gw = torch.zeros(nout, nin, device="cuda")
+        gb = torch.zeros(nout, device="cuda")
+        f = 2.0 * M * nout * nin
+        t = timeit(lambda: K.linear_dw_bias(dy, x, gw, gb), args.iters)
+        print(f"dW {name}: rows={M} nout={nout} nin={nin}  {t:7.3f} ms {f / t / 1e9:7.1f} TF/s", flush=True)
+        del dy, x, gw, gb
+        torch.cuda.empty_cache()
+
+
 def gemmk(args):
     """Fixed-cost probe: one output shape, growing K (fwd layout, bf16 out, bias)."""
     M, N = args.batch * 6272, 1152
@@ -135,7 +157,7 @@ def mbconv(args):
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["attn", "gemm", "gemmk", "mbconv"])
+    ap.add_argument("what", choices=["attn", "gemm", "gemmk", "mbconv", "dw"])
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--drop", type=float, default=0.1)
     ap.add_argument("--iters", type=int, default=5)
@@ -143,4 +165,4 @@ if __name__ == "__main__":
     a = ap.parse_args()
     from ssl_mae_amd.build import build
     build()
-    {"attn": attn, "gemm": gemm, "gemmk": gemmk, "mbconv": mbconv}[a.what](a)
+    {"attn": attn, "gemm": gemm, "gemmk": gemmk, "mbconv": mbconv, "dw": dw}[a.what](a)

@@ -50,9 +50,9 @@ struct GemmArgs {
 };
 
 template <typename TC>
-SM_DEV void epilogue_store(const GemmArgs& g, int64_t row, int col, float acc) {
+SM_DEV void epilogue_store(const GemmArgs& g, int64_t row, int col, float acc, int zs) {
   if (g.partial) {
-    g.partial[(int64_t)blockIdx.z * g.M * g.N + row * g.N + col] = acc;
+    g.partial[(int64_t)zs * g.M * g.N + row * g.N + col] = acc;
     return;
   }
   float v = g.alpha * acc;
@@ -189,10 +189,10 @@ SM_DEV void stage_put(const RowStage& rs, int region, int j, int p, int h, int l
 }
 
 // Epilogue of one wave's (32 MI) x (32 NJ) tile from the (swapped-operand) accumulators.  stage:
-// non-null -> RowStage stores (VEC, non-split-K path).
+// non-null -> RowStage stores (VEC, non-split-K path); zs: the split-K slab of this block.
 template <typename TC, bool VEC, int MI = 2, int NJ = 2>
 SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[MI][NJ], int m0, int n0,
-                                                         int wm, int wn, int l, char* stage = nullptr) {
+                                                         int wm, int wn, int l, int zs, char* stage = nullptr) {
   // The MFMAs run with swapped operands (D = B_frag x A_frag), so each lane owns
   // one output ROW (token) and registers r hold its columns
   // wn + 32j + (r&3) + 8(r>>2) + 4h: row-per-lane, no LDS round trip.
@@ -208,7 +208,7 @@ SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int col = n0 + wn + 32 * j + (r & 3) + 8 * (r >> 2) + 4 * h;
-          if (col < g.N) epilogue_store<TC>(g, row, col, acc[i][j][r]);
+          if (col < g.N) epilogue_store<TC>(g, row, col, acc[i][j][r], zs);
         }
     }
     return;
@@ -231,7 +231,7 @@ SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x
           acc[i][j][8 * p + 4 + e] = __uint_as_float(sw[1]);
         }
   if (g.partial) {   // split-K: raw fp32 runs into this z's slab
-    float* slab = g.partial + (int64_t)blockIdx.z * g.M * g.N;
+    float* slab = g.partial + (int64_t)zs * g.M * g.N;
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
       const int64_t row = rbase + 32 * i;
@@ -413,7 +413,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
     }
     __syncthreads();
   }
-  gemm_epilogue<TC, VEC>(g, acc, m0, n0, wm, wn, l);
+  gemm_epilogue<TC, VEC>(g, acc, m0, n0, wm, wn, l, blockIdx.z);
 }
 
 // ============================================================ bf16 MFMA kernel, v2
@@ -617,17 +617,22 @@ __global__ __launch_bounds__(BMV * 2, BMV == 256 ? 4 : 2) void gemm_bf16_v2(Gemm
   __shared__ __attribute__((aligned(16))) char lds[LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI];
   char* la = lds;
   char* lb = lds + BMV * BKT * 2;
+  // 1-D grid over (split zs, tile), split-major, with the bijective XCD remap: the
+  // n-tiles of one m-tile (sharing the A panel) and, under split-K, all tiles of one
+  // split (sharing its token rows of both operands) are dealt to one XCD's L2.
   const int ntn = (g.N + BNV - 1) / BNV;
+  const int ntiles = ntn * ((g.M + BMV - 1) / BMV);
   const int nwg = gridDim.x;
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int idx = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int zs = idx / ntiles, tile = idx - zs * ntiles;
   const int m0 = (tile / ntn) * BMV, n0 = (tile % ntn) * BNV;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
   const __bf16* A = (const __bf16*)g.A;
   const __bf16* B = (const __bf16*)g.B;
-  const int kb = g.k_begin + blockIdx.z * g.k_chunk;
+  const int kb = g.k_begin + zs * g.k_chunk;
   const int ke = min(g.K, kb + g.k_chunk);
 
   TileLoader<BMV, NT, AK> tla;
@@ -717,11 +722,11 @@ __global__ __launch_bounds__(BMV * 2, BMV == 256 ? 4 : 2) void gemm_bf16_v2(Gemm
       const int c = threadIdx.x, cg = c >> 3, j = c & 7;
       float sum = 0.f;
       for (int q = 0; q < NT / G; ++q) sum += red[(q * G + cg) * 8 + j];
-      if (m0 + c < g.M) g.colsum[(int64_t)blockIdx.z * g.M + m0 + c] = sum;
+      if (m0 + c < g.M) g.colsum[(int64_t)zs * g.M + m0 + c] = sum;
     }
     __syncthreads();
   }
-  gemm_epilogue<TC, VEC>(g, acc, m0, n0, wm, wn, l, lds + w * 8192);
+  gemm_epilogue<TC, VEC>(g, acc, m0, n0, wm, wn, l, zs, lds + w * 8192);
 }
 
 // ============================================================ f32 MFMA kernel
@@ -782,7 +787,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int64_t row = m0 + wm + (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (row < g.M) epilogue_store<float>(g, row, col, acc[r]);
+      if (row < g.M) epilogue_store<float>(g, row, col, acc[r], blockIdx.z);
     }
   }
 }
@@ -799,19 +804,49 @@ __global__ void splitk_reduce_kernel(GemmArgs g, int splits) {
     const int col = (int)(i - row * g.N);
     GemmArgs h = g;
     h.partial = nullptr;
-    epilogue_store<TC>(h, row, col, s);
+    epilogue_store<TC>(h, row, col, s, 0);
   }
 }
 
 int variant_bm(int v);
 int variant_bn(int v);
-int gemm_variant(int M, int N);
+int gemm_variant(int M, int N, int K);
+
+// Resident blocks of a bf16 variant on the whole device (occupancy query of the
+// split-K instantiation, cached; 2 / 4 blocks per CU x 256 CUs without a device).
+int gemm_slots(int v) {
+  static int cache[4] = {0, 0, 0, 0};
+  const int vi = v == 2 ? 2 : 3;
+  if (cache[vi]) return cache[vi];
+  int dev = 0, cus = 0, per = 0;
+  if (hipGetDevice(&dev) == hipSuccess &&
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess) {
+    const hipError_t e =
+        vi == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, gemm_bf16_v2<false, false, float, true, 256>, 512, 0)
+                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, gemm_bf16_v2<false, false, float, true, 128>, 256, 0);
+    if (e != hipSuccess) per = 0;
+  }
+  if (cus <= 0 || per <= 0) {
+    (void)hipGetLastError();
+    cus = 256;
+    per = vi == 2 ? 2 : 4;
+  }
+  cache[vi] = cus * per;
+  return cache[vi];
+}
+
+// Split-K over a long reduction (weight gradients: K = tokens).  bf16: the split count
+// makes the grid exactly two rounds of resident blocks (tiles x splits <= 2 x slots):
+// every block does the same work, so a grid one block past a round boundary pays a
+// whole extra round (the previous rule, ceil(1024 / tiles), gave 1026-1035 blocks for
+// 512 slots on every weight gradient of the step).
 int choose_splits(int M, int N, int K, bool bf16) {
-  const int v = gemm_variant(M, N);
+  const int v = gemm_variant(M, N, K);
   const int bm = bf16 ? variant_bm(v) : FBM, bn = bf16 ? variant_bn(v) : FBN, bk = bf16 ? BKT : FBK;
   const int64_t tiles = (int64_t)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
-  if (tiles >= 512 || K < 4096) return 1;
-  int64_t want = (1024 + tiles - 1) / tiles;
+  const int64_t slots = bf16 ? gemm_slots(v) : 512;
+  if (tiles >= slots || K < 4096) return 1;
+  int64_t want = bf16 ? (2 * slots) / tiles : (1024 + tiles - 1) / tiles;
   int64_t max_by_k = K / (4 * bk);
   int64_t s = want < max_by_k ? want : max_by_k;
   if (s > 2048) s = 2048;
@@ -819,12 +854,16 @@ int choose_splits(int M, int N, int K, bool bf16) {
 }
 
 // bf16 kernel variant: 1 = gemm_bf16_kernel (128 x 128, 4 waves), 2 = gemm_bf16_v2 at
-// BM = 256 (8 waves), 3 = gemm_bf16_v2 at BM = 128.  (A 256 x 256 tile fed by LDS-DMA,
-// double-buffered, 1 block / CU, measured 5-45 % slower than variant 2 on every
-// shape of the step, so it was dropped.)  Default (0): v2, BM = 256 when
+// BM = 256 (8 waves), 3 = gemm_bf16_v2 at BM = 128.  Default (0): v2, BM = 256 when
 // M >= 192 (a 256-row tile half empty loses to BM = 128 there: dW of the 96-channel
 // MBConv projection).  SM_GEMM_VARIANT pins one (A/B measurement runs).
-int gemm_variant(int M, int N) {
+// Measured and dropped (round 2): a 256 x 256 tile on 8 waves of 128 x 64 (0.75 KB of
+// fragment reads and 256 B of LDS-DMA staging per MFMA instead of v2's 1 KB + 384 B),
+// double-buffered buffer -> LDS DMA, one block per CU: 20-30 % slower than v2 on every
+// weight gradient of the step (profiles/r02g/dw_wide.txt).  Its operand delivery per CU
+// (64 KB in flight, ~21 GB/s) is the bound, not the LDS; v2's two resident blocks keep
+// 96 KB in flight.
+int gemm_variant(int M, int N, int K) {
   static const int forced = [] {
     const char* e = getenv("SM_GEMM_VARIANT");
     const int x = e ? atoi(e) : 0;
@@ -833,18 +872,19 @@ int gemm_variant(int M, int N) {
   if (forced) return forced;
   return M >= 192 ? 2 : 3;
   (void)N;
+  (void)K;
 }
 int variant_bm(int v) { return v == 2 ? 256 : 128; }
 int variant_bn(int v) { return 128; (void)v; }
 
 template <bool AK, bool BK, typename TC, bool VEC>
 void launch_bf16(const GemmArgs& g, int splits, hipStream_t st) {
-  const int v = gemm_variant(g.M, g.N);
+  const int v = gemm_variant(g.M, g.N, g.K);
   const int bm = variant_bm(v), bn = variant_bn(v);
-  dim3 grid(((g.N + bn - 1) / bn) * ((g.M + bm - 1) / bm), 1, splits);
-  if (v == 1) hipLaunchKernelGGL((gemm_bf16_kernel<AK, BK, TC, VEC>), grid, dim3(256), 0, st, g);
-  else if (v == 2) hipLaunchKernelGGL((gemm_bf16_v2<AK, BK, TC, VEC, 256>), grid, dim3(512), 0, st, g);
-  else hipLaunchKernelGGL((gemm_bf16_v2<AK, BK, TC, VEC, 128>), grid, dim3(256), 0, st, g);
+  const int tiles = ((g.N + bn - 1) / bn) * ((g.M + bm - 1) / bm);
+  if (v == 1) hipLaunchKernelGGL((gemm_bf16_kernel<AK, BK, TC, VEC>), dim3(tiles, 1, splits), dim3(256), 0, st, g);
+  else if (v == 2) hipLaunchKernelGGL((gemm_bf16_v2<AK, BK, TC, VEC, 256>), dim3(tiles * splits), dim3(512), 0, st, g);
+  else hipLaunchKernelGGL((gemm_bf16_v2<AK, BK, TC, VEC, 128>), dim3(tiles * splits), dim3(256), 0, st, g);
 }
 
 template <bool AK, bool BK>
@@ -872,9 +912,9 @@ int launch_layout(int abt, int ct, GemmArgs g, int splits, hipStream_t st) {
 // gradient: A = dy stored [K][M], fp32 split-K slabs)
 template <int IMP, typename TC>
 void launch_conv(const GemmArgs& g, int splits, hipStream_t st) {
-  const int v = gemm_variant(g.M, g.N) == 2 ? 2 : 3;
+  const int v = gemm_variant(g.M, g.N, 0) == 2 ? 2 : 3;
   const int bm = variant_bm(v);
-  dim3 grid(((g.N + 127) / 128) * ((g.M + bm - 1) / bm), 1, splits);
+  dim3 grid(((g.N + 127) / 128) * ((g.M + bm - 1) / bm) * splits);
   constexpr bool AK = IMP == 1, BK = IMP == 1;
   if (v == 2) hipLaunchKernelGGL((gemm_bf16_v2<AK, BK, TC, true, 256, IMP>), grid, dim3(512), 0, st, g);
   else hipLaunchKernelGGL((gemm_bf16_v2<AK, BK, TC, true, 128, IMP>), grid, dim3(256), 0, st, g);
@@ -1035,7 +1075,7 @@ extern "C" int sm_linear_dw_bias(int rows, int nout, int nin, const void* dy, co
                                  int accumulate, void* ws, int64_t ws_bytes, hipStream_t stream) {
   if (nout <= 0 || nin <= 0) return 0;
   if (ws_bytes < sm_linear_dw_bias_workspace_bytes(rows, nout, nin)) return -4;
-  if (gemm_variant(nout, nin) == 1 || nout % 8 || nin % 8) return -2;   // the row sums live in the v2 kernel
+  if (gemm_variant(nout, nin, rows) == 1 || nout % 8 || nin % 8) return -2;   // the row sums live in the v2 kernel
   const int s = choose_splits(nout, nin, rows, true);
   const int64_t gbytes = s > 1 ? (int64_t)s * nout * nin * 4 : 0;
   float* colsum = (float*)(((uintptr_t)ws + gbytes + 15) & ~(uintptr_t)15);

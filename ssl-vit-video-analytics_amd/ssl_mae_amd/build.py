@@ -45,8 +45,13 @@ def build(verbose=False, jobs=None):
     srcs = _sources()
     objs = [os.path.join(BUILD, os.path.basename(s) + ".o") for s in srcs]
 
+    headers = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(INCLUDE, "*.h"))
+    hdr_t = max(os.path.getmtime(f) for f in headers) if headers else 0.0
+
     def compile_one(pair):
         src, obj = pair
+        if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hdr_t):
+            return obj   # object up to date with its source and every header
         cmd = [HIPCC] + FLAGS + FILE_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:

@@ -45,7 +45,9 @@ def rnd(*shape, dtype=torch.float32, scale=1.0, seed=0):
 # ------------------------------------------------------------------ GEMM
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("la,lb", [(0, 0), (0, 1), (1, 0), (1, 1)])
-@pytest.mark.parametrize("M,N,K", [(200, 72, 96), (1000, 384, 192), (64, 1152, 384), (256, 96, 8)])
+@pytest.mark.parametrize("M,N,K", [(200, 72, 96), (1000, 384, 192), (64, 1152, 384), (256, 96, 8),
+                                   # long K with ragged M / N tiles and K tails (not a multiple of 64)
+                                   (296, 200, 1088), (520, 96, 1040), (64, 1152, 1024), (768, 512, 1536)])
 def test_gemm_layouts(dtype, la, lb, M, N, K):
     A = rnd(M, K, dtype=dtype, seed=1)
     Bm = rnd(K, N, dtype=dtype, seed=2)
@@ -58,8 +60,9 @@ def test_gemm_layouts(dtype, la, lb, M, N, K):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_gemm_epilogues(dtype):
-    M, N, Kd = 300, 192, 128
+@pytest.mark.parametrize("Kd", [128, 1536])
+def test_gemm_epilogues(dtype, Kd):
+    M, N = 300, 192
     x = rnd(M, Kd, dtype=dtype, seed=3)
     w = rnd(N, Kd, dtype=dtype, seed=4, scale=0.1)
     b = rnd(N, seed=5)
@@ -600,7 +603,7 @@ def test_linear_dx_gelu_backward_epilogue(dtype, p):
     assert rel_err(got, pr.grad) < tol
 
 
-@pytest.mark.parametrize("M", [98, 49, 1001])
+@pytest.mark.parametrize("M", [98, 49, 1001, 1100, 4099])
 def test_weight_grad_any_row_count(M):
     """dW = dy^T x over a token-row count that is not a multiple of 8 (fine-tune
     per-frame calls: B * 7 * 7 rows): both operands M/N-major, K tail zero-filled."""
