@@ -47,6 +47,15 @@ int sm_gemm(int ab_dtype, int c_dtype, int a_layout, int b_layout, int M, int N,
 int64_t sm_linear_dw_bias_workspace_bytes(int rows, int nout, int nin);
 int sm_linear_dw_bias(int rows, int nout, int nin, const void* dy, const void* x, float* dW, float* db,
                       int accumulate, void* ws, int64_t ws_bytes, hipStream_t stream);
+/* fc2's weight gradient with the activation formed in the GEMM's operand loads:
+ * dW[nout][nin] (+)= dy^T dropout(GELU(pre)), db += colsum(dy); pre = the fc1
+ * pre-activation [rows][nin] bf16, (drop_p, seed) the fc1 output's dropout (the Mlp of
+ * tiny_vit.py:74-84, the decoder feed-forward).  Bit-identical to sm_gelu_fwd followed by
+ * sm_linear_dw_bias without the recompute pass; workspace as
+ * sm_linear_dw_bias_workspace_bytes. */
+int sm_linear_dw_bias_gelu(int rows, int nout, int nin, const void* dy, const void* pre, float drop_p,
+                           uint64_t seed, float* dW, float* db, int accumulate, void* ws, int64_t ws_bytes,
+                           hipStream_t stream);
 
 /* ---- fused attention (tiny_vit.py:103 F.scaled_dot_product_attention;
  * torch MultiheadAttention core of the decoder, mae_vit_adapter.py:40-48).

@@ -94,6 +94,28 @@ def dw(args):
         torch.cuda.empty_cache()
 
 
+def dwx(args):
+    """fc2 weight gradients of dropout(GELU(pre)) (linear_dw_bias gelu=) against the gelu
+    recompute kernel + plain weight gradient; outputs compared bitwise."""
+    B = args.batch
+    dev = "cuda"
+    for name, M, H, nout, p in [("dec fc2", B * 6272, 1536, 384, 0.1), ("s2 fc2", B * 8 * 784, 1536, 384, 0.0),
+                                ("s1 fc2", B * 8 * 3136, 768, 192, 0.0)]:
+        pre = torch.randn(M, H, device=dev).to(torch.bfloat16)
+        dy = (torch.randn(M, nout, device=dev) * 0.1).to(torch.bfloat16)
+        gw1, gb1 = torch.zeros(nout, H, device=dev), torch.zeros(nout, device=dev)
+        gw2, gb2 = torch.zeros(nout, H, device=dev), torch.zeros(nout, device=dev)
+        K.linear_dw_bias(dy, K.gelu(pre, p, 77), gw1, gb1)
+        K.linear_dw_bias(dy, pre, gw2, gb2, gelu=(p, 77))
+        same = torch.equal(gw1, gw2) and torch.equal(gb1, gb2)
+        t0 = timeit(lambda: K.linear_dw_bias(dy, K.gelu(pre, p, 77), gw1, gb1), args.iters)
+        t1 = timeit(lambda: K.linear_dw_bias(dy, pre, gw2, gb2, gelu=(p, 77)), args.iters)
+        print(f"{name}: rows={M} dW[{nout}][{H}] p={p}  gelu kernel + dW {t0:7.3f} ms | dW(gelu=) {t1:7.3f} ms | "
+              f"bit-identical {same}", flush=True)
+        del pre, dy
+        torch.cuda.empty_cache()
+
+
 def gemmk(args):
     """Fixed-cost probe: one output shape, growing K (fwd layout, bf16 out, bias)."""
     M, N = args.batch * 6272, 1152
@@ -157,7 +179,7 @@ def mbconv(args):
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["attn", "gemm", "gemmk", "mbconv", "dw"])
+    ap.add_argument("what", choices=["attn", "gemm", "gemmk", "mbconv", "dw", "dwx"])
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--drop", type=float, default=0.1)
     ap.add_argument("--iters", type=int, default=5)
@@ -165,4 +187,4 @@ if __name__ == "__main__":
     a = ap.parse_args()
     from ssl_mae_amd.build import build
     build()
-    {"attn": attn, "gemm": gemm, "gemmk": gemmk, "mbconv": mbconv, "dw": dw}[a.what](a)
+    {"attn": attn, "gemm": gemm, "gemmk": gemmk, "mbconv": mbconv, "dw": dw, "dwx": dwx}[a.what](a)

@@ -47,6 +47,9 @@ struct GemmArgs {
   // tap * cC + c with tap = ky * 3 + kx, source pixel = pixel + (ky-1, kx-1), or
   // + (1-ky, 1-kx) when cflip (data gradient).  Pixels outside the frame read zero.
   int cH, cW, cC, cflip;
+  // weight-gradient B operand formed on load (IMP 5, XformColsB): dropout after the GELU
+  float xb_p;
+  uint64_t xb_seed;
 };
 
 template <typename TC>
@@ -608,11 +611,71 @@ struct ConvColsB {
   }
 };
 
+// Weight-gradient B operand formed on load (IMP 5).  B(k, n) = dropout(GELU(x[k][n]))
+// with x the fc1 pre-activation stored [K = token rows][N] (M/N-major) and the fc1
+// output's keep mask, formed per 16-B chunk in the staging registers on its way to LDS
+// and rounded to bf16 exactly as the gelu kernel stores it, so the fc2 weight gradient
+// is bit-identical to recompute-then-GEMM without the recompute pass (read pre, write
+// h, read h back).  Rows past K and columns past N read zero.  Pays when the weight
+// gradient has one m-tile (nout <= 256: every B chunk activated once); with two the
+// activation runs twice per element and the recompute pass is cheaper (kernels.py).
+// (A LayerNorm form of this operand -- the qkv / fc1 weight gradients without the LN
+// recompute -- measured neutral: its extra registers force 2 waves / SIMD, which costs
+// what the recompute pass did.)
+template <int ROWS, int NT>
+struct XformColsB {
+  static constexpr int CH = ROWS * 64 * 2 / 16 / NT;
+  static constexpr int KSTEP = NT / (ROWS / 8);
+  uint32_t voff[CH];
+  int loff0, kk0, col;
+  uint4 raw[CH];
+  SM_DEV void init(const GemmArgs& g, int n0) {
+    const int t = threadIdx.x;
+    kk0 = t / (ROWS / 8);
+    col = (t % (ROWS / 8)) * 8;
+    loff0 = mnmaj_off_r<ROWS>(kk0, col);
+#pragma unroll
+    for (int i = 0; i < CH; ++i)
+      voff[i] = n0 + col < g.N ? (uint32_t)(((int64_t)(kk0 + KSTEP * i) * g.ldb + col) * 2) : BUF_OOB;
+  }
+  // K-step at k0 (absolute token row); kvalid rows left
+  SM_DEV void load(const GemmArgs& g, int n0, int k0, int kvalid) {
+    const __bf16* xb = (const __bf16*)g.B + (int64_t)k0 * g.ldb + n0;
+    const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)xb, (short)0, (int)BUF_OOB, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const uint32_t o = kk0 + KSTEP * i < kvalid ? voff[i] : BUF_OOB;
+      raw[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, o, 0, 0));
+    }
+  }
+  SM_DEV void store(char* lds, const GemmArgs& g, int n0, int k0) const {
+    const uint32_t thr = drop_thr(g.xb_p);
+    const float ks = g.xb_p > 0.f ? 1.f / (1.f - g.xb_p) : 1.f;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      float x[8], v[8];
+      load8((const __bf16*)&raw[i], x);
+      const uint32_t rb = drop_rowbase(seed32(g.xb_seed), (uint64_t)(k0 + kk0 + KSTEP * i));
+#pragma unroll
+      for (int e4 = 0; e4 < 8; e4 += 4) {   // = gelu_fwd_kernel / drop_mult8
+        const uint32_t h = g.xb_p > 0.f ? drop_hash(rb, (uint32_t)(n0 + col + e4)) : 0xFFFFFFFFu;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          v[e4 + e] = gelu_f(x[e4 + e]) * (g.xb_p > 0.f ? (((h >> (8 * e)) & 0xFFu) >= thr ? ks : 0.f) : 1.f);
+      }
+      *(uint4*)(lds + loff0 + i * KSTEP * ROWS * 2) = pack8(v, (__bf16*)nullptr);
+    }
+  }
+};
+
 // IMP: 0 plain operands; 1 A is the implicit im2col of a conv (ConvRowsA);
-// 2 B is (ConvColsB).
+// 2 B is (ConvColsB); 5 B is formed on load (XformColsB).
+// (IMP 5: the activation's registers do not fit beside the staging set at 4 waves /
+// SIMD -- scratch spills inside the K loop -- so it runs at 2 waves / SIMD.)
 template <bool AK, bool BK, typename TC, bool VEC, int BMV, int IMP = 0>
-__global__ __launch_bounds__(BMV * 2, BMV == 256 ? 4 : 2) void gemm_bf16_v2(GemmArgs g) {
+__global__ __launch_bounds__(BMV * 2, (BMV == 256 && IMP != 5) ? 4 : 2) void gemm_bf16_v2(GemmArgs g) {
   constexpr int NT = BMV * 2, BNV = 128;
+  constexpr bool XB = IMP == 5;
   constexpr int LDS_MAIN = (BMV + BNV) * BKT * 2, LDS_EPI = (NT / 64) * 8192;   // operand tiles | row stage
   __shared__ __attribute__((aligned(16))) char lds[LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI];
   char* la = lds;
@@ -639,10 +702,13 @@ __global__ __launch_bounds__(BMV * 2, BMV == 256 ? 4 : 2) void gemm_bf16_v2(Gemm
   TileLoader<BNV, NT, BK> tlb;
   ConvRowsA<BMV, NT> cla;
   ConvColsB<BNV, NT> clb;
+  XformColsB<BNV, NT> xlb;
   if constexpr (IMP == 1) cla.init(g, m0, kb);
   else tla.init(g.lda, g.M - m0);
   if constexpr (IMP == 2) clb.init(g, n0, kb);
+  else if constexpr (XB) xlb.init(g, n0);
   else tlb.init(g.ldb, g.N - n0);
+
   // element offset of K-step k0 of each panel
   const int64_t abase = AK ? (int64_t)m0 * g.lda : (int64_t)m0;
   const int64_t bbase = BK ? (int64_t)n0 * g.ldb : (int64_t)n0;
@@ -656,6 +722,7 @@ __global__ __launch_bounds__(BMV * 2, BMV == 256 ? 4 : 2) void gemm_bf16_v2(Gemm
   };
   auto load_b = [&](int k0, uint4 (&r)[TileLoader<BNV, NT, BK>::CH]) {
     if constexpr (IMP == 2) clb.load(panel_rsrc(B, (int64_t)k0 * g.cC + cbase), g, ke - k0, r);
+    else if constexpr (XB) xlb.load(g, n0, k0, ke - k0);
     else tlb.load(panel_rsrc(B, bbase + k0 * bstep), ke - k0, r);
   };
 
@@ -691,6 +758,7 @@ __global__ __launch_bounds__(BMV * 2, BMV == 256 ? 4 : 2) void gemm_bf16_v2(Gemm
     if constexpr (IMP == 1) cla.store(la, ra);
     else tla.store(la, ra);
     if constexpr (IMP == 2) clb.store(lb, rb);
+    else if constexpr (XB) xlb.store(lb, g, n0, k0);
     else tlb.store(lb, rb);
     __syncthreads();
     if (k0 + BKT < ke) {
@@ -839,7 +907,9 @@ int gemm_slots(int v) {
 // makes the grid exactly two rounds of resident blocks (tiles x splits <= 2 x slots):
 // every block does the same work, so a grid one block past a round boundary pays a
 // whole extra round (the previous rule, ceil(1024 / tiles), gave 1026-1035 blocks for
-// 512 slots on every weight gradient of the step).
+// 512 slots on every weight gradient of the step).  (A group-major order -- each
+// split's tiles sharing a token range dealt consecutively in groups of <= 8 -- measured
+// 0-16 % slower than this split-major order on every weight gradient.)
 int choose_splits(int M, int N, int K, bool bf16) {
   const int v = gemm_variant(M, N, K);
   const int bm = bf16 ? variant_bm(v) : FBM, bn = bf16 ? variant_bn(v) : FBN, bk = bf16 ? BKT : FBK;
@@ -1069,6 +1139,50 @@ extern "C" int sm_gemm(int ab_dtype, int c_dtype, int a_layout, int b_layout, in
 extern "C" int64_t sm_linear_dw_bias_workspace_bytes(int rows, int nout, int nin) {
   const int s = choose_splits(nout, nin, rows, true);
   return (s > 1 ? (int64_t)s * nout * nin * 4 : 0) + (int64_t)s * nout * 4 + 256;
+}
+
+// fc2's weight gradient dW[nout][nin] (+)= dy^T dropout(GELU(pre)), db += colsum(dy),
+// with the activation formed in the GEMM's operand loads (XformColsB): pre is the fc1
+// pre-activation [rows][nin] bf16, (drop_p, seed) the fc1 output's dropout.
+extern "C" int sm_linear_dw_bias_gelu(int rows, int nout, int nin, const void* dy, const void* pre, float drop_p,
+                                      uint64_t seed, float* dW, float* db, int accumulate, void* ws, int64_t ws_bytes,
+                                      hipStream_t stream) {
+  if (nout <= 0 || nin <= 0 || rows <= 0) return 0;
+  if (ws_bytes < sm_linear_dw_bias_workspace_bytes(rows, nout, nin)) return -4;
+  if (nout % 8 || nin % 8 || (((uintptr_t)dy | (uintptr_t)pre) & 15)) return -2;
+  const int v = gemm_variant(nout, nin, rows);
+  if (v == 1) return -2;
+  const int s = choose_splits(nout, nin, rows, true);
+  const int64_t gbytes = s > 1 ? (int64_t)s * nout * nin * 4 : 0;
+  float* colsum = (float*)(((uintptr_t)ws + gbytes + 15) & ~(uintptr_t)15);
+  GemmArgs g{};
+  g.M = nout; g.N = nin; g.K = rows; g.A = dy; g.lda = nout; g.B = pre; g.ldb = nin; g.C = dW; g.ldc = nin;
+  g.alpha = 1.f; g.beta = accumulate ? 1.f : 0.f; g.rows_per_group = 1; g.colsum = colsum;
+  g.xb_p = drop_p; g.xb_seed = seed;
+  int splits = s;
+  if (splits > 1) {
+    int chunk = (rows + splits - 1) / splits;
+    chunk = (chunk + BKT - 1) / BKT * BKT;
+    splits = (rows + chunk - 1) / chunk;
+    g.k_begin = 0; g.k_chunk = chunk; g.partial = (float*)ws;
+  } else {
+    g.k_begin = 0; g.k_chunk = rows;
+  }
+  const int bm = variant_bm(v);
+  const dim3 grid(((nin + 127) / 128) * ((nout + bm - 1) / bm) * splits);
+  if (v == 2) hipLaunchKernelGGL((gemm_bf16_v2<false, false, float, true, 256, 5>), grid, dim3(512), 0, stream, g);
+  else hipLaunchKernelGGL((gemm_bf16_v2<false, false, float, true, 128, 5>), grid, dim3(256), 0, stream, g);
+  SM_CHECK_LAUNCH();
+  if (splits > 1) {
+    const int64_t total = (int64_t)nout * nin;
+    int blocks = (int)((total + 255) / 256);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(splitk_reduce_kernel<float>, dim3(blocks), dim3(256), 0, stream, g, splits);
+    SM_CHECK_LAUNCH();
+  }
+  colred(colsum, splits, nout, nullptr, db, 1, stream);
+  SM_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int sm_linear_dw_bias(int rows, int nout, int nin, const void* dy, const void* x, float* dW, float* db,

@@ -326,6 +326,7 @@ class BlockFn(torch.autograd.Function):
         st = ctx.st
         mode = st.mode
         act = mode.act
+        rb = mode.bf16
         N, L, H, D = st.N, st.L, st.heads, st.head_dim
         _touch(*ctx.params)
         dout = dout.contiguous()
@@ -334,9 +335,12 @@ class BlockFn(torch.autograd.Function):
         db = dout if dout.dtype == act else K.cast(dout, act)       # grad of the bf16 branch
         if st.drop2 > 0 or st.dp2 is not None:
             db = K.dropout_bwd(db, st.drop2, st.seed2, st.dp2, L)
-        h = K.gelu(hpre, st.drop_ff, st.seed_ff)
-        K.linear_dw_bias(db, h, G(w2), G(b2))
-        del h
+        if rb:   # fc2 weight gradient of dropout(GELU(hpre)) (kernels.linear_dw_bias picks the form)
+            K.linear_dw_bias(db, hpre, G(w2), G(b2), gelu=(st.drop_ff, st.seed_ff))
+        else:
+            h = K.gelu(hpre, st.drop_ff, st.seed_ff)
+            K.linear_dw_bias(db, h, G(w2), G(b2))
+            del h
         # dL/dhpre straight from the fc2 data-gradient GEMM's epilogue (keep mask and
         # GELU' applied there: no dh round trip, no gelu_bwd pass)
         dhpre = K.linear_dx(db, W(w2, mode), gelu_pre=hpre, drop_p=st.drop_ff, seed=st.seed_ff)

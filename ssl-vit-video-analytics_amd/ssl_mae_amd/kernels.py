@@ -77,11 +77,24 @@ def linear_dw(dy, x, grad_sink, accumulate=True):
     return grad_sink
 
 
-def linear_dw_bias(dy, x, grad_w, grad_b):
-    """grad_w[N,K] += dy^T @ x and grad_b[N] += sum over rows of dy.  bf16: one GEMM
-    whose n0 == 0 blocks also sum dy (sm_linear_dw_bias); fp32 (parity): two ops."""
+def linear_dw_bias(dy, x, grad_w, grad_b, gelu=None):
+    """grad_w[N,K] += dy^T @ x' and grad_b[N] += sum over rows of dy.  bf16: one GEMM
+    whose n0 == 0 blocks also sum dy (sm_linear_dw_bias); fp32 (parity): two ops.
+    x' = x, or with gelu=(drop_p, seed) x' = dropout(GELU(x)) of the fc1 pre-activation
+    x: formed in the GEMM's operand loads (sm_linear_dw_bias_gelu) when the weight
+    gradient has one 256-row tile (N <= 256), else by the gelu kernel first (two
+    m-tiles would activate every element twice; the recompute pass is cheaper)."""
     M, N = dy.shape
     K = x.shape[1]
+    if gelu is not None:
+        if (N <= 256 and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and N % 8 == 0 and K % 8 == 0):
+            _chk(dy, x, grad_w, grad_b)
+            nbytes = query("sm_linear_dw_bias_workspace_bytes", M, N, K)
+            ws = _ws(nbytes, dy.device)
+            call("sm_linear_dw_bias_gelu", M, N, K, ptr(dy), ptr(x), float(gelu[0]), int(gelu[1]), ptr(grad_w),
+                 ptr(grad_b), 1, ptr(ws), nbytes, stream())
+            return grad_w
+        return linear_dw_bias(dy, gelu_fwd(x, gelu[0], gelu[1]), grad_w, grad_b)
     if dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and N % 8 == 0 and K % 8 == 0:
         _chk(dy, x, grad_w, grad_b)
         nbytes = query("sm_linear_dw_bias_workspace_bytes", M, N, K)
@@ -192,6 +205,10 @@ def bn_bwd(dy, x2d, mean, rstd, w, b, gelu, dw_sink, db_sink, row_scale=None, ro
 
 # ------------------------------------------------------------------ elementwise
 def gelu(x, drop_p=0.0, seed=0):
+    return gelu_fwd(x, drop_p, seed)
+
+
+def gelu_fwd(x, drop_p=0.0, seed=0):
     y = torch.empty_like(x)
     call("sm_gelu_fwd", dt(x), x.numel(), x.shape[-1], ptr(x), ptr(y), float(drop_p), int(seed), stream())
     return y

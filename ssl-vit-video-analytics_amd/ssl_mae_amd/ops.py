@@ -159,9 +159,21 @@ def _linear_dw_bias(dy, x, grad_w, grad_b):
 _linear_dw_bias.register_fake(_none)
 
 
-def linear_dw_bias(dy, x, grad_w, grad_b):
-    torch.ops.ssl_mae.linear_dw_bias(dy, x, grad_w, grad_b)
+def linear_dw_bias(dy, x, grad_w, grad_b, gelu=None):
+    if gelu is not None:
+        torch.ops.ssl_mae.linear_dw_bias_gelu(dy, x, grad_w, grad_b, float(gelu[0]), _s64(gelu[1]))
+    else:
+        torch.ops.ssl_mae.linear_dw_bias(dy, x, grad_w, grad_b)
     return grad_w
+
+
+@_op("linear_dw_bias_gelu", "(Tensor dy, Tensor pre, Tensor(a!) grad_w, Tensor(b!) grad_b, float drop_p, "
+                            "int seed) -> ()", ("grad_w", "grad_b"))
+def _linear_dw_bias_gelu(dy, pre, grad_w, grad_b, drop_p, seed):
+    _K.linear_dw_bias(dy, pre, grad_w, grad_b, gelu=(drop_p, _u64(seed)))
+
+
+_linear_dw_bias_gelu.register_fake(_none)
 
 
 @_op("colsum", "(Tensor x, Tensor(a!) out, bool accumulate) -> ()", ("out",))

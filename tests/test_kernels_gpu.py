@@ -683,3 +683,24 @@ def test_conv3x3_implicit_gemm(Fn, H, W, Cin, Cout):
     g = torch.zeros(Cout, Cin, 3, 3, device=DEV)
     kk.conv_wunpack_add(dwp - 0.5, g, 1)
     assert rel_err(g, wr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("M,N,H,p", [(70000, 256, 1536, 0.1), (70000, 192, 768, 0.0), (1001, 96, 64, 0.1),
+                                     (70000, 384, 1536, 0.1)])
+def test_linear_dw_bias_gelu_operand(M, N, H, p):
+    """fc2's weight gradient of dropout(GELU(pre)): with the activation formed in the
+    GEMM's operand loads (N <= 256, no recompute pass) or through the gelu kernel (N =
+    384), bit-identical to gelu() + linear_dw_bias(), and the fp32 torch math of the
+    same mask."""
+    kk = KK()
+    pre = rnd(M, H, dtype=torch.bfloat16, seed=170).to(DEV)
+    dy = rnd(M, N, dtype=torch.bfloat16, seed=171, scale=0.1).to(DEV)
+    h = kk.gelu(pre, p, 99)
+    gw1, gb1 = torch.zeros(N, H, device=DEV), torch.zeros(N, device=DEV)
+    gw2, gb2 = gw1.clone(), gb1.clone()
+    kk.linear_dw_bias(dy, h, gw1, gb1)
+    kk.linear_dw_bias(dy, pre, gw2, gb2, gelu=(p, 99))
+    assert torch.equal(gw1, gw2) and torch.equal(gb1, gb2)
+    keep = ((h.float() != 0) | (kk.gelu(pre).float() == 0)).float()
+    ref = dy.float().t() @ (F.gelu(pre.float()) * keep / (1 - p))
+    assert rel_err(gw2, ref) < 2e-2
