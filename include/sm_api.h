@@ -168,6 +168,12 @@ int sm_dwconv_bn_bwd(int F, int H, int W, int C, const void* dy, const void* x, 
                      const float* bn_rstd, const float* bn_w, const float* bn_b, int bn_gelu, const float* w,
                      void* dx, float* dw, float* dgamma, float* dbeta, void* ws, int64_t ws_bytes,
                      hipStream_t st);
+/* Stride-2 form (the MBConv opening stages 1-3): F, H, W, C are the input's, dy is
+ * [F][(H-1)/2+1][(W-1)/2+1][C]; same outputs and workspace (sm_dwconv_bn_bwd_workspace_bytes). */
+int sm_dwconv_s2_bn_bwd(int F, int H, int W, int C, const void* dy, const void* x, const float* bn_mean,
+                        const float* bn_rstd, const float* bn_w, const float* bn_b, int bn_gelu, const float* w,
+                        void* dx, float* dw, float* dgamma, float* dbeta, void* ws, int64_t ws_bytes,
+                        hipStream_t st);
 int sm_dwconv_bwd(int dtype, const void* dy, const void* x, const float* w, void* dx, float* dw, int F,
                   int H, int W, int C, int stride, void* ws, int64_t ws_bytes, hipStream_t st);
 

@@ -165,6 +165,14 @@ def mbconv(args):
     rep("dwconv_bn_bwd s1 (2 passes)", timeit(lambda: K.dwconv_bn_bwd(y, a, act, w, dw, g0, b0, Fn, H, W, C),
                                               args.iters), 5)
     rep("dwconv_fused s2", timeit(lambda: K.dwconv_fused(a, act, w, Fn, H, W, C, 2), args.iters), 1.25)
+    y2 = K.dwconv_fused(a, act, w, Fn, H, W, C, 2)
+    rep("s2 bwd unfused (dw bwd+bn_bwd)", timeit(lambda: K.bn_bwd(K.dwconv_fused_bwd(y2, a, act, w, dw, Fn, H, W, C, 2),
+                                                                  a, m, r, g, b, True, torch.zeros(C, device=dev),
+                                                                  torch.zeros(C, device=dev)), args.iters), 5.25)
+    rep("dwconv_bn_bwd s2 (2 passes)", timeit(lambda: K.dwconv_bn_bwd(y2, a, act, w, dw, torch.zeros(C, device=dev),
+                                                                       torch.zeros(C, device=dev), Fn, H, W, C,
+                                                                       stride=2), args.iters), 4.25)
+    del y2
     w1 = torch.randn(C // 4, C, device=dev) * 0.1
     w2 = torch.randn(C, C // 4, device=dev) * 0.1
     _, _, h1, sg = K.se_fwd(a, Fn, H * W, C, w1, w2, act=act, want_y=False)

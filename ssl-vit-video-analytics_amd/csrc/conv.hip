@@ -280,9 +280,9 @@ constexpr int DWF_CB = 32, DWF_PX = 7, DWF_KV = 7;
 template <int S>
 constexpr int dwf_ty() { return S == 1 ? 4 : 2; }
 
-template <int S>
+template <int S, int TY_ = dwf_ty<S>()>
 struct DwRing {
-  static constexpr int TY = dwf_ty<S>();
+  static constexpr int TY = TY_;
   static constexpr int NR = (TY - 1) * S + 3;
   static constexpr int NEW = TY * S;              // rows entering the ring per band
   const __bf16* x;
@@ -695,6 +695,176 @@ __global__ __launch_bounds__(256, 2) void dwb_kernel(const __bf16* dy, const __b
           }
         }
         __builtin_amdgcn_sched_barrier(0);   // one tap row's reads in flight at a time (VGPR budget)
+      }
+      float mu[4], rs[4];
+      load4(cl + 2 * DWF_CB + c4 * 4, mu);
+      load4(cl + 3 * DWF_CB + c4 * 4, rs);
+#pragma unroll
+      for (int p = 0; p < PX; ++p) {
+        float d[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          d[j] = (float)(__bf16)(g[p][j] * gg[p][j]);   // the stored dz: the sums see what dx will
+          sdz[j] += d[j];
+          sdzx[j] = fmaf(d[j], ((float)xs[p][j] - mu[j]) * rs[j], sdzx[j]);
+        }
+        bf16x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = (__bf16)d[j];
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, o), zr, off0 + p * C * 2, 0, 0);
+      }
+    }
+  }
+  __syncthreads();                     // ring dead: reuse for the reductions
+  float* red = (float*)lds;            // [256][4]
+  auto reduce = [&](const float* v4, float* dst, int64_t stride) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[t * 4 + j] = v4[j];
+    __syncthreads();
+    if (t < DWF_CB) {
+      const int cc = t >> 2, j = t & 3;
+      float s = 0.f;
+      for (int k = 0; k < 32; ++k) s += red[(k * 8 + cc) * 4 + j];
+      dst[(int64_t)t * stride] = s;
+    }
+    __syncthreads();
+  };
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) reduce(dwa[tap], part_w + (f * C + cs * DWF_CB) * 9 + tap, 9);
+  reduce(sdz, part_bn + (f * 2 + 0) * C + cs * DWF_CB, 1);
+  reduce(sdzx, part_bn + (f * 2 + 1) * C + cs * DWF_CB, 1);
+}
+
+// Stride-2 form of dwb_kernel (the MBConv that opens stages 1-3: tiny_vit.py:46 with
+// stride 2).  The input pixel (yi, xi) receives dy[yo][xo] w[ky][kx] for the taps with
+// yi + 1 - ky = 2 yo and xi + 1 - kx = 2 xo: one tap row for even yi (ky = 1), two for
+// odd yi (ky = 0, 2), and likewise along x -- 2.25 taps per pixel, each also feeding
+// dw[ky][kx] += dy h.  The ring holds dy rows (output resolution, zero halo; rows past
+// Ho read zero): a band of 2 DWB2_TYO = 4 input rows needs dy rows yo0 .. yo0 + 2, two
+// of them new.  Thread = 4 channels x DWB2_PX = 4 input pixels of one row (an even
+// strip start, so the x tap pattern is fixed per pixel: even p one column, odd p two).
+// Replaces depthwise dgrad (dh1 written at input resolution), the fused depthwise
+// weight gradient and the BatchNorm/GELU backward's two passes over (dh1, x): dy read
+// once, x twice, dz written and read once, GELU evaluated once per element.
+constexpr int DWB2_PX = 4, DWB2_TYO = 2, DWB2_PAD = 2 * 64;
+
+template <bool GELU>
+__global__ __launch_bounds__(256, 2) void dwb2_kernel(const __bf16* dy, const __bf16* x, ChanAffine bn,
+                                                      const float* w, __bf16* dz, float* part_w, float* part_bn,
+                                                      int H, int W, int C, int Ho, int Wo, int remap) {
+  using R = DwRing<1, DWB2_TYO>;
+  constexpr int TYI = 2 * DWB2_TYO;      // input rows per band
+  constexpr int PX = DWB2_PX;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const DwfBlock blk(C / DWF_CB, remap);
+  const int cs = blk.cs;
+  const int64_t f = blk.f;
+  const int t = threadIdx.x;
+  R ring{dy, f, Ho, Wo, C, cs * DWF_CB + (t & 3) * 8, t & 3, (Wo + 2) * 64};
+  Affine8 raw;
+  raw.init(ChanAffine{nullptr, nullptr, nullptr, nullptr, 0}, 0);
+  const int c4 = t & 7;
+  const int c0 = cs * DWF_CB + c4 * 4;
+  // a ragged last strip's pixels past W read up to two columns past the last ring row:
+  // zero pad, so those values (which only meet h = GELU' = 0) are never NaN bit patterns
+  char* pad = lds + R::NR * ring.pitch;
+  if (t < DWB2_PAD / 16) *(uint4*)(pad + 16 * t) = make_uint4(0, 0, 0, 0);
+  float* wl = (float*)(pad + DWB2_PAD);              // taps wl[tap][ch] = w[ch][tap]
+  for (int i = t; i < 9 * DWF_CB; i += 256) {
+    const int tap = i / DWF_CB, ch = i % DWF_CB;
+    wl[i] = w[(int64_t)(cs * DWF_CB + ch) * 9 + tap];
+  }
+  float* cl = wl + 9 * DWF_CB;                      // BN constants [4][32]: scale, shift, mean, rstd
+  if (t < DWF_CB) {
+    const int c = cs * DWF_CB + t;
+    const float r = bn.rstd[c], scv = r * bn.w[c];
+    cl[t] = scv;
+    cl[DWF_CB + t] = bn.b[c] - bn.mean[c] * scv;
+    cl[2 * DWF_CB + t] = bn.mean[c];
+    cl[3 * DWF_CB + t] = r;
+  }
+  float dwa[9][4], sdz[4], sdzx[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    sdz[j] = sdzx[j] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) dwa[k][j] = 0.f;
+  }
+  const int nstrip = (W + PX - 1) / PX;
+  const int items = TYI * nstrip;
+  const int nbands = (H + TYI - 1) / TYI;
+  ring.stage_first<true>(lds, raw);
+  for (int band = 0; band < nbands; ++band) {
+    const int y0 = band * TYI, yo0 = band * DWB2_TYO;
+    if (band > 0) {
+      __syncthreads();
+      ring.commit<true>(lds, raw, yo0 + 1, R::NEW);
+    }
+    __syncthreads();
+    if (band + 1 < nbands) ring.load<true>(yo0 + DWB2_TYO + 1, R::NEW);
+#pragma unroll 1
+    for (int it = t >> 3; it < items; it += 32) {
+      const int ry = it / nstrip, strip = it - ry * nstrip;
+      const int yi = y0 + ry;
+      if (yi >= H) continue;
+      const int xi0 = strip * PX;
+      const int64_t row0 = (f * H + yi) * W;
+      const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)(x + row0 * C), (short)0, W * C * 2, 0x00020000);
+      const auto zr = __builtin_amdgcn_make_buffer_rsrc((void*)(dz + row0 * C), (short)0, W * C * 2, 0x00020000);
+      const uint32_t off0 = (uint32_t)(xi0 * C + c0) * 2u;
+      float h[PX][4], gg[PX][4], g[PX][4];
+      bf16x4 xs[PX];
+      {
+        float sc[4], sh[4];
+        load4(cl + c4 * 4, sc);
+        load4(cl + DWF_CB + c4 * 4, sh);
+#pragma unroll
+        for (int p = 0; p < PX; ++p)
+          xs[p] = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(xr, off0 + p * C * 2, 0, 0));
+#pragma unroll
+        for (int p = 0; p < PX; ++p) {
+          const bool ok = xi0 + p < W;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float u = fmaf((float)xs[p][j], sc[j], sh[j]);
+            float cdf = 1.f, pdf = 0.f;
+            if (GELU) cdf = gelu_phi_pair(u, &pdf);
+            h[p][j] = ok ? (float)(__bf16)(GELU ? u * cdf : u) : 0.f;
+            gg[p][j] = ok ? fmaf(u, pdf, cdf) : 0.f;
+            g[p][j] = 0.f;
+          }
+          __builtin_amdgcn_sched_barrier(0);   // bound the interleaved GELU chains (VGPR budget)
+        }
+      }
+      // one tap row ky over dy row yo: LDS columns xi0 / 2 + cj + 1, cj = 0..4 feed pixel
+      // 2cj (kx = 1), 2cj - 1 (kx = 0) and 2cj + 1 (kx = 2)
+      auto tap_row = [&](int ky, int yo) {
+        const char* rowp = lds + ring.slot(yo) * ring.pitch + c4 * 8 + (xi0 / 2 + 1) * 64;
+        float wr[3][4];
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) load4(wl + (ky * 3 + kx) * DWF_CB + c4 * 4, wr[kx]);
+#pragma unroll
+        for (int cj = 0; cj <= PX / 2; ++cj) {
+          float v[4];
+          load4((const __bf16*)(rowp + cj * 64), v);
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) {
+            const int p = 2 * cj + kx - 1;   // xi0 + p + 1 - kx = 2 (xi0 / 2 + cj)
+            if (p < 0 || p >= PX) continue;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              g[p][j] = fmaf(v[j], wr[kx][j], g[p][j]);
+              dwa[ky * 3 + kx][j] = fmaf(v[j], h[p][j], dwa[ky * 3 + kx][j]);
+            }
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      if (yi & 1) {
+        tap_row(0, (yi + 1) >> 1);
+        tap_row(2, (yi - 1) >> 1);
+      } else {
+        tap_row(1, yi >> 1);
       }
       float mu[4], rs[4];
       load4(cl + 2 * DWF_CB + c4 * 4, mu);
@@ -1300,11 +1470,16 @@ extern "C" int64_t sm_dwconv_bn_bwd_workspace_bytes(int F, int H, int W, int C) 
   return ((int64_t)F * C * 9 + (int64_t)F * 2 * C + 2 * C) * 4 + 2 * C * 8 + 64;
 }
 
-extern "C" int sm_dwconv_bn_bwd(int F, int H, int W, int C, const void* dy, const void* x, const float* bn_mean,
-                                const float* bn_rstd, const float* bn_w, const float* bn_b, int bn_gelu,
-                                const float* w, void* dx, float* dw, float* dgamma, float* dbeta, void* ws,
-                                int64_t ws_bytes, hipStream_t st) {
-  if (!dwf_shape_ok(F, W, C, 1) || !bn_mean || !dx || dwf_lds_bytes(W, 1) + DWB_PAD + 4 * DWF_CB * 4 > 64 * 1024) return -2;
+static int dwconv_bn_bwd(int stride, int F, int H, int W, int C, const void* dy, const void* x, const float* bn_mean,
+                         const float* bn_rstd, const float* bn_w, const float* bn_b, int bn_gelu, const float* w,
+                         void* dx, float* dw, float* dgamma, float* dbeta, void* ws, int64_t ws_bytes,
+                         hipStream_t st) {
+  const int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
+  size_t lds = stride == 1 ? dwf_lds_bytes(W, 1) + DWB_PAD + 4 * DWF_CB * 4
+                           : (size_t)DwRing<1, DWB2_TYO>::NR * (Wo + 2) * 64 + DWB2_PAD + 13 * DWF_CB * 4;
+  if (lds < 256 * 4 * 4) lds = 256 * 4 * 4;   // the reductions reuse it ([256][4] floats)
+  if (!dwf_shape_ok(F, W, C, stride) || !bn_mean || !dx || lds > 64 * 1024) return -2;
+  if (stride == 2 && DwRing<1, DWB2_TYO>::NEW * Wo * 4 > 256 * DWF_KV) return -2;
   if (((uintptr_t)x & 15) || ((uintptr_t)dy & 15) || ((uintptr_t)dx & 15) || C / 8 > 256) return -2;
   if (ws_bytes < sm_dwconv_bn_bwd_workspace_bytes(F, H, W, C)) return -4;
   float* part_w = (float*)ws;
@@ -1313,13 +1488,20 @@ extern "C" int sm_dwconv_bn_bwd(int F, int H, int W, int C, const void* dy, cons
   double* sums = (double*)(((uintptr_t)(coef + 2 * C) + 7) & ~(uintptr_t)7);
   ChanAffine bn{bn_mean, bn_rstd, bn_w, bn_b, bn_gelu};
   const dim3 grid((C / DWF_CB) * F);
-  const size_t lds = dwf_lds_bytes(W, 1) + DWB_PAD + 4 * DWF_CB * 4;
-  if (bn_gelu)
+  if (stride == 2) {
+    if (bn_gelu)
+      hipLaunchKernelGGL(dwb2_kernel<true>, grid, dim3(256), lds, st, (const __bf16*)dy, (const __bf16*)x, bn, w,
+                         (__bf16*)dx, part_w, part_bn, H, W, C, Ho, Wo, dwf_remap());
+    else
+      hipLaunchKernelGGL(dwb2_kernel<false>, grid, dim3(256), lds, st, (const __bf16*)dy, (const __bf16*)x, bn, w,
+                         (__bf16*)dx, part_w, part_bn, H, W, C, Ho, Wo, dwf_remap());
+  } else if (bn_gelu) {
     hipLaunchKernelGGL(dwb_kernel<true>, grid, dim3(256), lds, st, (const __bf16*)dy, (const __bf16*)x, bn, w,
                        (__bf16*)dx, part_w, part_bn, H, W, C, dwf_remap());
-  else
+  } else {
     hipLaunchKernelGGL(dwb_kernel<false>, grid, dim3(256), lds, st, (const __bf16*)dy, (const __bf16*)x, bn, w,
                        (__bf16*)dx, part_w, part_bn, H, W, C, dwf_remap());
+  }
   colred(part_w, F, C * 9, nullptr, dw, 1, st);
   colred(part_bn, F, 2 * C, sums, nullptr, 0, st);
   const int64_t M = (int64_t)F * H * W;
@@ -1331,6 +1513,23 @@ extern "C" int sm_dwconv_bn_bwd(int F, int H, int W, int C, const void* dy, cons
                      (const float*)coef, (__bf16*)dx, M, C, (int)rpb);
   SM_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int sm_dwconv_bn_bwd(int F, int H, int W, int C, const void* dy, const void* x, const float* bn_mean,
+                                const float* bn_rstd, const float* bn_w, const float* bn_b, int bn_gelu,
+                                const float* w, void* dx, float* dw, float* dgamma, float* dbeta, void* ws,
+                                int64_t ws_bytes, hipStream_t st) {
+  return dwconv_bn_bwd(1, F, H, W, C, dy, x, bn_mean, bn_rstd, bn_w, bn_b, bn_gelu, w, dx, dw, dgamma, dbeta, ws,
+                       ws_bytes, st);
+}
+
+// Stride-2 form (dwb2_kernel): F, H, W, C are the input's; dy is [F][Ho][Wo][C].
+extern "C" int sm_dwconv_s2_bn_bwd(int F, int H, int W, int C, const void* dy, const void* x, const float* bn_mean,
+                                   const float* bn_rstd, const float* bn_w, const float* bn_b, int bn_gelu,
+                                   const float* w, void* dx, float* dw, float* dgamma, float* dbeta, void* ws,
+                                   int64_t ws_bytes, hipStream_t st) {
+  return dwconv_bn_bwd(2, F, H, W, C, dy, x, bn_mean, bn_rstd, bn_w, bn_b, bn_gelu, w, dx, dw, dgamma, dbeta, ws,
+                       ws_bytes, st);
 }
 
 extern "C" int64_t sm_dwconv_wgrad_workspace_bytes(int F, int H, int W, int C, int stride) {

@@ -77,6 +77,7 @@ _SIGS = {
     "sm_dwconv_fused_bwd": (_c_i32, [_c_i32] * 5 + [_c_p] * 6 + [_c_i32] + [_c_p] * 4 + [_c_i64, _c_p]),
     "sm_dwconv_bn_bwd_workspace_bytes": (_c_i64, [_c_i32] * 4),
     "sm_dwconv_bn_bwd": (_c_i32, [_c_i32] * 4 + [_c_p] * 6 + [_c_i32] + [_c_p] * 6 + [_c_i64, _c_p]),
+    "sm_dwconv_s2_bn_bwd": (_c_i32, [_c_i32] * 4 + [_c_p] * 6 + [_c_i32] + [_c_p] * 6 + [_c_i64, _c_p]),
     "sm_bn_eval_params": (_c_i32, [_c_p, _c_p, _c_i32, _c_f32, _c_p, _c_p, _c_p]),
     "sm_segment_mean": (_c_i32, [_c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p]),
     "sm_segment_mean_bwd": (_c_i32, [_c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_p, _c_p]),

@@ -263,16 +263,12 @@ class MBConvFn(torch.autograd.Function):
         K.gemm(dz1, pooled, G(w_fc0), R, mid, Fr, 1, 1, R, mid, mid, beta=1.0)
         if a1 is None:
             a1 = K.linear(x.reshape(-1, Cin), W(w_exp, mode).view(mid, Cin))
-        if ctx.fused and s == 1:
+        if ctx.fused:
             # depthwise + BN0/GELU backward in two passes over (da2, a1); dh1 never stored
             act0 = (m0, r0, g0.detach(), b0.detach(), True)
             da1 = K.dwconv_bn_bwd(da2, a1, act0, w_dw.detach().view(mid, 9), G(w_dw).view(mid, 9), G(g0), G(b0),
-                                  Fr, H, Wd, mid)
+                                  Fr, H, Wd, mid, stride=s)
             dh1 = None
-        elif ctx.fused:
-            act0 = (m0, r0, g0.detach(), b0.detach(), True)
-            dh1 = K.dwconv_fused_bwd(da2, a1, act0, w_dw.detach().view(mid, 9), G(w_dw).view(mid, 9), Fr, H, Wd,
-                                     mid, s)
         else:
             h1 = K.bn_apply(a1, m0, r0, g0.detach(), b0.detach(), gelu=True)
             dh1 = K.dwconv_bwd(da2, h1, w_dw.detach().view(mid, 9), G(w_dw).view(mid, 9), Fr, H, Wd, mid, s)

@@ -402,16 +402,16 @@ def dwconv_fused_bwd(dy, x, act, w, dw_sink, F, H, W, C, stride, need_dx=True):
     return dx
 
 
-def dwconv_bn_bwd(dy, x, act, w, dw_sink, dg_sink, db_sink, F, H, W, C):
-    """Stride-1 y = dwconv3x3(act(x)), act = GELU(BN(x)) with batch statistics
+def dwconv_bn_bwd(dy, x, act, w, dw_sink, dg_sink, db_sink, F, H, W, C, stride=1):
+    """y = dwconv3x3(act(x), stride 1 or 2), act = GELU(BN(x)) with batch statistics
     (act = (mean, rstd, gamma, beta, gelu)): returns dL/dx; dw_sink, dg_sink, db_sink
-    += dL/dw, dL/dgamma, dL/dbeta (bf16)."""
+    += dL/dw, dL/dgamma, dL/dbeta (bf16).  F, H, W, C: the input's."""
     _chk(dy, x)
     dx = torch.empty_like(x)
     nbytes = query("sm_dwconv_bn_bwd_workspace_bytes", F, H, W, C)
     ws = _ws(nbytes, x.device)
     a = _act_args(act)
-    call("sm_dwconv_bn_bwd", F, H, W, C, ptr(dy), ptr(x), a[0], a[1], a[2], a[3], a[4], ptr(w), ptr(dx),
+    call("sm_dwconv_s2_bn_bwd" if stride == 2 else "sm_dwconv_bn_bwd", F, H, W, C, ptr(dy), ptr(x), a[0], a[1], a[2], a[3], a[4], ptr(w), ptr(dx),
          ptr(dw_sink), ptr(dg_sink), ptr(db_sink), ptr(ws), nbytes, stream())
     return dx
 

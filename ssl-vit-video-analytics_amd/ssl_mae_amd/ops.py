@@ -648,16 +648,16 @@ def dwconv_fused_bwd(dy, x, act, w, dw_sink, F, H, W, C, stride, need_dx=True):
 
 @_op("dwconv_bn_bwd", "(Tensor dy, Tensor x, Tensor bn_mean, Tensor bn_rstd, Tensor bn_w, Tensor bn_b, "
                       "bool bn_gelu, Tensor w, Tensor(a!) dw_sink, Tensor(b!) dg_sink, Tensor(c!) db_sink, int F, "
-                      "int H, int W, int C) -> Tensor", ("dw_sink", "dg_sink", "db_sink"))
-def _dwconv_bn_bwd(dy, x, bm, br, bw, bb, bg, w, dw_sink, dg_sink, db_sink, F, H, W, C):
-    return _K.dwconv_bn_bwd(dy, x, (bm, br, bw, bb, bg), w, dw_sink, dg_sink, db_sink, F, H, W, C)
+                      "int H, int W, int C, int stride=1) -> Tensor", ("dw_sink", "dg_sink", "db_sink"))
+def _dwconv_bn_bwd(dy, x, bm, br, bw, bb, bg, w, dw_sink, dg_sink, db_sink, F, H, W, C, stride=1):
+    return _K.dwconv_bn_bwd(dy, x, (bm, br, bw, bb, bg), w, dw_sink, dg_sink, db_sink, F, H, W, C, stride)
 
 
 _dwconv_bn_bwd.register_fake(lambda dy, x, *a: torch.empty_like(x))
 
 
-def dwconv_bn_bwd(dy, x, act, w, dw_sink, dg_sink, db_sink, F, H, W, C):
-    return torch.ops.ssl_mae.dwconv_bn_bwd(dy, x, *_act(act), w, dw_sink, dg_sink, db_sink, F, H, W, C)
+def dwconv_bn_bwd(dy, x, act, w, dw_sink, dg_sink, db_sink, F, H, W, C, stride=1):
+    return torch.ops.ssl_mae.dwconv_bn_bwd(dy, x, *_act(act), w, dw_sink, dg_sink, db_sink, F, H, W, C, int(stride))
 
 
 # ============================================================================ SE

@@ -267,13 +267,14 @@ def test_mbconv_fused_middle_vs_fp32_torch(Fr, H, C, stride):
     # reference's autocast backward: 3e-2, like da1
     for got, ref, nm in ((dg0, tg0.grad, "bn0.w"), (db0, tb0.grad, "bn0.b")):
         assert rel(got, ref) < 3e-2, nm
-    if stride == 1:
-        # the two-pass depthwise + BN0/GELU backward (sm_dwconv_bn_bwd) the stride-1
-        # MBConvs run: same references, and close to the unfused sequence above
+    if True:
+        # the two-pass depthwise + BN0/GELU backward (sm_dwconv_bn_bwd / sm_dwconv_s2_bn_bwd)
+        # the MBConvs run: same references, and close to the unfused sequence above
+        # (odd shapes of the stride-2 form: test_kernels_gpu.py::test_dwconv_bn_bwd_vs_fp32)
         dwdw_b = torch.zeros(C, 9, device=DEV)
         dg0_b = torch.zeros(C, device=DEV)
         db0_b = torch.zeros(C, device=DEV)
-        da1_b = kk.dwconv_bn_bwd(da2, a1, act0, wdw, dwdw_b, dg0_b, db0_b, Fr, H, W, C)
+        da1_b = kk.dwconv_bn_bwd(da2, a1, act0, wdw, dwdw_b, dg0_b, db0_b, Fr, H, W, C, stride=stride)
         torch.cuda.synchronize()
         assert rel(da1_b, xa.grad) < 3e-2
         assert rel(da1_b, da1) < 2e-2

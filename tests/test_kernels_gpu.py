@@ -704,3 +704,39 @@ def test_linear_dw_bias_gelu_operand(M, N, H, p):
     keep = ((h.float() != 0) | (kk.gelu(pre).float() == 0)).float()
     ref = dy.float().t() @ (F.gelu(pre.float()) * keep / (1 - p))
     assert rel_err(gw2, ref) < 2e-2
+
+
+@pytest.mark.parametrize("Fr,H,C,s", [(4, 19, 64, 2), (4, 20, 64, 2), (3, 30, 32, 2), (2, 56, 768, 2),
+                                      (4, 7, 1536, 2), (4, 4, 768, 2), (4, 8, 384, 2),
+                                      (4, 19, 64, 1), (2, 112, 96, 1)])
+def test_dwconv_bn_bwd_vs_fp32(Fr, H, C, s):
+    """The fused depthwise + BatchNorm0/GELU backward (sm_dwconv_bn_bwd, stride 1;
+    sm_dwconv_s2_bn_bwd, stride 2: odd and even sizes, ragged last strips, the zero
+    dy row past Ho) against fp32 autograd of conv2d(GELU(batch_norm(x)), groups=C) from
+    the same bf16 inputs, and against the unfused sequence (depthwise backward, then
+    bn_bwd)."""
+    kk = KK()
+    W = H
+    Ho = (H - 1) // s + 1
+    a1 = (rnd(Fr * H * W, C, seed=180, scale=1.5) + 0.2).to(torch.bfloat16).to(DEV)
+    g0 = (rnd(C, seed=181, scale=0.2) + 1.0).to(DEV)
+    b0 = rnd(C, seed=182, scale=0.2).to(DEV)
+    wdw = rnd(C, 9, seed=183, scale=0.3).to(DEV)
+    m0, r0 = kk.bn_stats(a1)
+    act0 = (m0, r0, g0, b0, True)
+    da2 = rnd(Fr * Ho * Ho, C, dtype=torch.bfloat16, seed=184, scale=1e-2).to(DEV)
+    dw_f = torch.zeros(C, 9, device=DEV)
+    dg_f, db_f = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    da1 = kk.dwconv_bn_bwd(da2, a1, act0, wdw, dw_f, dg_f, db_f, Fr, H, W, C, stride=s)
+    dw_u = torch.zeros(C, 9, device=DEV)
+    dh1 = kk.dwconv_fused_bwd(da2, a1, act0, wdw, dw_u, Fr, H, W, C, s)
+    dg_u, db_u = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    da1_u = kk.bn_bwd(dh1, a1, m0, r0, g0, b0, True, dg_u, db_u)
+    x = a1.float().view(Fr, H, W, C).permute(0, 3, 1, 2).contiguous().requires_grad_(True)
+    tg, tb, tw = g0.clone().requires_grad_(True), b0.clone().requires_grad_(True), wdw.clone().requires_grad_(True)
+    y = F.conv2d(F.gelu(F.batch_norm(x, None, None, tg, tb, True, 0.0, 1e-5)), tw.view(C, 1, 3, 3), None, s, 1, 1, C)
+    y.backward(da2.float().view(Fr, Ho, Ho, C).permute(0, 3, 1, 2))
+    gx = x.grad.permute(0, 2, 3, 1).reshape(-1, C)
+    assert rel_err(da1, gx) < 2e-2 and rel_err(da1, da1_u) < 2e-2
+    assert rel_err(dw_f, tw.grad) < 1e-2 and rel_err(dw_f, dw_u) < 1e-2
+    assert rel_err(dg_f, tg.grad) < 2e-2 and rel_err(db_f, tb.grad) < 2e-2
