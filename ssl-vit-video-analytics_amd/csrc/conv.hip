@@ -272,8 +272,8 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(const T* dy, const float*
 // (zero border columns; rows outside the image are zero: the convolution pads
 // act(x)).  Each input row is transformed once; the TY*S new rows of band b+1 are
 // loaded into registers while band b is computed (software pipeline).  Every thread
-// computes PX = 7 consecutive outputs x 8 channels per item; odd PX keeps the 16-lane
-// groups of ds_read_b128 conflict-free (strip pitch 448 B).  Taps accumulate in the
+// computes PX = 7 consecutive outputs x 8 channels per item at stride 1 (odd PX keeps
+// the 16-lane groups of ds_read_b128 conflict-free: strip pitch 448 B), 2 at stride 2.  Taps accumulate in the
 // (ky, kx) order of dw_fwd_kernel: bit-identical y.
 constexpr int DWF_CB = 32, DWF_PX = 7, DWF_KV = 7;
 
@@ -377,7 +377,9 @@ __global__ __launch_bounds__(256, 2) void dwf_fwd_kernel(const __bf16* x, ChanAf
                                                          int Wo, int remap) {
   using R = DwRing<S>;
   constexpr int TY = R::TY;
-  constexpr int PX = DWF_PX;
+  // stride 2: 2 outputs per item (a band of TY = 2 rows x Wo / 7 strips x 4 chunks left
+  // three of the four waves idle while one computed; 2 keeps 88 % of the block busy)
+  constexpr int PX = S == 1 ? DWF_PX : 2;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const DwfBlock blk(C / DWF_CB, remap);
   const int cs = blk.cs;
