@@ -56,6 +56,17 @@ int sm_linear_dw_bias(int rows, int nout, int nin, const void* dy, const void* x
 int sm_linear_dw_bias_gelu(int rows, int nout, int nin, const void* dy, const void* pre, float drop_p,
                            uint64_t seed, float* dW, float* db, int accumulate, void* ws, int64_t ws_bytes,
                            hipStream_t stream);
+/* The MBConv projection's weight gradient over the SE output (tiny_vit.py:29-34, 53,
+ * replacing the Conv2d weight-gradient autograd node fed by SELayer.forward's product):
+ * dW[nout][nin] (+)= dy^T h3, h3[r][c] = bf16(bf16(act(a2[r][c])) * gate[r / hw][c]),
+ * act = BatchNorm(mean, rstd, w, b) + GELU (act_gelu) of the depthwise output a2
+ * [rows][nin] bf16, gate [rows / hw][nin] fp32 (the SE sigmoid), dy [rows][nout] bf16,
+ * fp32 dW.  h3 is formed in the GEMM's operand loads exactly as sm_se_scale stores it:
+ * bit-identical to sm_se_scale + sm_gemm.  hw % 64 == 0. */
+int64_t sm_linear_dw_se_workspace_bytes(int rows, int nout, int nin);
+int sm_linear_dw_se(int rows, int nout, int nin, const void* dy, const void* a2, const float* act_mean,
+                    const float* act_rstd, const float* act_w, const float* act_b, int act_gelu, const float* gate,
+                    int hw, float* dW, int accumulate, void* ws, int64_t ws_bytes, hipStream_t stream);
 
 /* ---- fused attention (tiny_vit.py:103 F.scaled_dot_product_attention;
  * torch MultiheadAttention core of the decoder, mae_vit_adapter.py:40-48).

@@ -116,6 +116,33 @@ def dwx(args):
         torch.cuda.empty_cache()
 
 
+def dwse(args):
+    """MBConv projection weight gradient over the SE output: se_scale + linear_dw against
+    linear_dw_se (h3 formed in the GEMM's operand loads); outputs compared bitwise."""
+    B = args.batch
+    dev = "cuda"
+    for name, Fn, HW, N, C in [("s0 proj", B * 8, 12544, 96, 384), ("s1 down proj", B * 8, 3136, 192, 384)]:
+        M = Fn * HW
+        a2 = (torch.randn(M, C, device=dev) * 2).to(torch.bfloat16)
+        dy = (torch.randn(M, N, device=dev) * 0.1).to(torch.bfloat16)
+        act = (torch.zeros(C, device=dev), torch.ones(C, device=dev), torch.ones(C, device=dev),
+               torch.zeros(C, device=dev), True)
+        gate = torch.rand(Fn, C, device=dev)
+        g1, g2 = torch.zeros(N, C, device=dev), torch.zeros(N, C, device=dev)
+
+        def unfused():
+            K.linear_dw(dy, K.se_scale(a2, gate, Fn, HW, C, act=act), g1, accumulate=False)
+        unfused()
+        K.linear_dw_se(dy, a2, act, gate, HW, g2, accumulate=False)
+        same = torch.equal(g1, g2)
+        t0 = timeit(unfused, args.iters)
+        t1 = timeit(lambda: K.linear_dw_se(dy, a2, act, gate, HW, g2, accumulate=False), args.iters)
+        print(f"{name}: rows={M} dW[{N}][{C}]  se_scale + dW {t0:7.3f} ms | dW(se operand) {t1:7.3f} ms | "
+              f"bit-identical {same}", flush=True)
+        del a2, dy
+        torch.cuda.empty_cache()
+
+
 def gemmk(args):
     """Fixed-cost probe: one output shape, growing K (fwd layout, bf16 out, bias)."""
     M, N = args.batch * 6272, 1152
@@ -187,7 +214,7 @@ def mbconv(args):
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["attn", "gemm", "gemmk", "mbconv", "dw", "dwx"])
+    ap.add_argument("what", choices=["attn", "gemm", "gemmk", "mbconv", "dw", "dwx", "dwse"])
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--drop", type=float, default=0.1)
     ap.add_argument("--iters", type=int, default=5)
@@ -195,4 +222,4 @@ if __name__ == "__main__":
     a = ap.parse_args()
     from ssl_mae_amd.build import build
     build()
-    {"attn": attn, "gemm": gemm, "gemmk": gemmk, "mbconv": mbconv, "dw": dw, "dwx": dwx}[a.what](a)
+    {"attn": attn, "gemm": gemm, "gemmk": gemmk, "mbconv": mbconv, "dw": dw, "dwx": dwx, "dwse": dwse}[a.what](a)

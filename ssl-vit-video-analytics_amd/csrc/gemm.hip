@@ -47,9 +47,14 @@ struct GemmArgs {
   // tap * cC + c with tap = ky * 3 + kx, source pixel = pixel + (ky-1, kx-1), or
   // + (1-ky, 1-kx) when cflip (data gradient).  Pixels outside the frame read zero.
   int cH, cW, cC, cflip;
-  // weight-gradient B operand formed on load (IMP 5, XformColsB): dropout after the GELU
+  // weight-gradient B operand formed on load (XformColsB): IMP 5 dropout after the GELU
   float xb_p;
   uint64_t xb_seed;
+  // IMP 7: the SE output act(x) * gate[frame][n] with act = the BatchNorm + GELU of the
+  // stored pre-activation (ChanAffine) and xb_hw token rows per frame
+  ChanAffine xb_act;
+  const float* xb_gate;
+  int xb_hw;
 };
 
 template <typename TC>
@@ -622,13 +627,23 @@ struct ConvColsB {
 // (A LayerNorm form of this operand -- the qkv / fc1 weight gradients without the LN
 // recompute -- measured neutral: its extra registers force 2 waves / SIMD, which costs
 // what the recompute pass did.)
-template <int ROWS, int NT>
+// (IMP 7, sm_linear_dw_se: the MBConv projection's weight gradient over the SE output
+// h3 = bf16(bf16(GELU(BN2(a2))) * gate[frame][c]), formed per chunk exactly as
+// se_apply_kernel stores it -- bit-identical to se_scale + GEMM without the h3 round trip.
+// The per-column BN affine stays in registers (a thread's columns are fixed); each
+// 64-row K-step lies in one frame (host: xb_hw % 64 == 0, split chunks multiples of 64),
+// so the gate is one 8-float run per K-step, prefetched with the operand.  Rows past K
+// are zeroed after the transform: GELU(BN(0)) is not 0.)
+template <int ROWS, int NT, int IMP>
 struct XformColsB {
   static constexpr int CH = ROWS * 64 * 2 / 16 / NT;
   static constexpr int KSTEP = NT / (ROWS / 8);
   uint32_t voff[CH];
   int loff0, kk0, col;
   uint4 raw[CH];
+  uint32_t kvalid_mask;
+  float gt[IMP == 7 ? 8 : 1];
+  Affine8 af;
   SM_DEV void init(const GemmArgs& g, int n0) {
     const int t = threadIdx.x;
     kk0 = t / (ROWS / 8);
@@ -637,45 +652,64 @@ struct XformColsB {
 #pragma unroll
     for (int i = 0; i < CH; ++i)
       voff[i] = n0 + col < g.N ? (uint32_t)(((int64_t)(kk0 + KSTEP * i) * g.ldb + col) * 2) : BUF_OOB;
+    if constexpr (IMP == 7) af.init(g.xb_act, n0 + col < g.N ? n0 + col : 0);
   }
   // K-step at k0 (absolute token row); kvalid rows left
   SM_DEV void load(const GemmArgs& g, int n0, int k0, int kvalid) {
     const __bf16* xb = (const __bf16*)g.B + (int64_t)k0 * g.ldb + n0;
     const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)xb, (short)0, (int)BUF_OOB, 0x00020000);
+    kvalid_mask = 0;
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
-      const uint32_t o = kk0 + KSTEP * i < kvalid ? voff[i] : BUF_OOB;
-      raw[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, o, 0, 0));
+      const bool ok = kk0 + KSTEP * i < kvalid;
+      kvalid_mask |= ok ? 1u << i : 0u;
+      raw[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, ok ? voff[i] : BUF_OOB, 0, 0));
+    }
+    if constexpr (IMP == 7) {
+      const int c = n0 + col < g.N ? n0 + col : 0;
+      load8(g.xb_gate + (int64_t)(k0 / g.xb_hw) * g.N + c, gt);
     }
   }
   SM_DEV void store(char* lds, const GemmArgs& g, int n0, int k0) const {
-    const uint32_t thr = drop_thr(g.xb_p);
-    const float ks = g.xb_p > 0.f ? 1.f / (1.f - g.xb_p) : 1.f;
+    if constexpr (IMP == 7) {
 #pragma unroll
-    for (int i = 0; i < CH; ++i) {
-      float x[8], v[8];
-      load8((const __bf16*)&raw[i], x);
-      const uint32_t rb = drop_rowbase(seed32(g.xb_seed), (uint64_t)(k0 + kk0 + KSTEP * i));
+      for (int i = 0; i < CH; ++i) {
+        float v[8];
+        load8((const __bf16*)&raw[i], v);
+        af.apply<__bf16>(v);   // = se_apply_kernel: act rounded to bf16, then * gate
 #pragma unroll
-      for (int e4 = 0; e4 < 8; e4 += 4) {   // = gelu_fwd_kernel / drop_mult8
-        const uint32_t h = g.xb_p > 0.f ? drop_hash(rb, (uint32_t)(n0 + col + e4)) : 0xFFFFFFFFu;
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          v[e4 + e] = gelu_f(x[e4 + e]) * (g.xb_p > 0.f ? (((h >> (8 * e)) & 0xFFu) >= thr ? ks : 0.f) : 1.f);
+        for (int j = 0; j < 8; ++j) v[j] = (kvalid_mask >> i) & 1u ? v[j] * gt[j] : 0.f;
+        *(uint4*)(lds + loff0 + i * KSTEP * ROWS * 2) = pack8(v, (__bf16*)nullptr);
       }
-      *(uint4*)(lds + loff0 + i * KSTEP * ROWS * 2) = pack8(v, (__bf16*)nullptr);
+    } else {
+      const uint32_t thr = drop_thr(g.xb_p);
+      const float ks = g.xb_p > 0.f ? 1.f / (1.f - g.xb_p) : 1.f;
+#pragma unroll
+      for (int i = 0; i < CH; ++i) {
+        float x[8], v[8];
+        load8((const __bf16*)&raw[i], x);
+        const uint32_t rb = drop_rowbase(seed32(g.xb_seed), (uint64_t)(k0 + kk0 + KSTEP * i));
+#pragma unroll
+        for (int e4 = 0; e4 < 8; e4 += 4) {   // = gelu_fwd_kernel / drop_mult8
+          const uint32_t h = g.xb_p > 0.f ? drop_hash(rb, (uint32_t)(n0 + col + e4)) : 0xFFFFFFFFu;
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            v[e4 + e] = gelu_f(x[e4 + e]) * (g.xb_p > 0.f ? (((h >> (8 * e)) & 0xFFu) >= thr ? ks : 0.f) : 1.f);
+        }
+        *(uint4*)(lds + loff0 + i * KSTEP * ROWS * 2) = pack8(v, (__bf16*)nullptr);
+      }
     }
   }
 };
 
 // IMP: 0 plain operands; 1 A is the implicit im2col of a conv (ConvRowsA);
-// 2 B is (ConvColsB); 5 B is formed on load (XformColsB).
+// 2 B is (ConvColsB); 5 / 7 B is formed on load (XformColsB).
 // (IMP 5: the activation's registers do not fit beside the staging set at 4 waves /
 // SIMD -- scratch spills inside the K loop -- so it runs at 2 waves / SIMD.)
 template <bool AK, bool BK, typename TC, bool VEC, int BMV, int IMP = 0>
-__global__ __launch_bounds__(BMV * 2, (BMV == 256 && IMP != 5) ? 4 : 2) void gemm_bf16_v2(GemmArgs g) {
+__global__ __launch_bounds__(BMV * 2, (BMV == 256 && IMP != 5 && IMP != 7) ? 4 : 2) void gemm_bf16_v2(GemmArgs g) {
   constexpr int NT = BMV * 2, BNV = 128;
-  constexpr bool XB = IMP == 5;
+  constexpr bool XB = IMP == 5 || IMP == 7;
   constexpr int LDS_MAIN = (BMV + BNV) * BKT * 2, LDS_EPI = (NT / 64) * 8192;   // operand tiles | row stage
   __shared__ __attribute__((aligned(16))) char lds[LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI];
   char* la = lds;
@@ -702,7 +736,7 @@ __global__ __launch_bounds__(BMV * 2, (BMV == 256 && IMP != 5) ? 4 : 2) void gem
   TileLoader<BNV, NT, BK> tlb;
   ConvRowsA<BMV, NT> cla;
   ConvColsB<BNV, NT> clb;
-  XformColsB<BNV, NT> xlb;
+  XformColsB<BNV, NT, IMP> xlb;
   if constexpr (IMP == 1) cla.init(g, m0, kb);
   else tla.init(g.lda, g.M - m0);
   if constexpr (IMP == 2) clb.init(g, n0, kb);
@@ -1182,6 +1216,54 @@ extern "C" int sm_linear_dw_bias_gelu(int rows, int nout, int nin, const void* d
   }
   colred(colsum, splits, nout, nullptr, db, 1, stream);
   SM_CHECK_LAUNCH();
+  return 0;
+}
+
+// The MBConv projection's weight gradient over the SE output (tiny_vit.py:29-34, 53):
+// dW[nout][nin] (+)= dy^T h3 with h3[r][c] = bf16(bf16(GELU(a2[r][c] sc[c] + sh[c])) *
+// gate[r / hw][c]) formed in the B-operand loads (IMP 7): se_scale's h3 pass (read a2,
+// write h3, read it back) disappears.  a2 [rows][nin] bf16, dy [rows][nout] bf16;
+// rows = frames * hw with hw % 64 == 0 (each 64-row K-step inside one frame).
+extern "C" int64_t sm_linear_dw_se_workspace_bytes(int rows, int nout, int nin) {
+  const int s = choose_splits(nout, nin, rows, true);
+  return s > 1 ? (int64_t)s * nout * nin * 4 : 16;
+}
+
+extern "C" int sm_linear_dw_se(int rows, int nout, int nin, const void* dy, const void* a2, const float* act_mean,
+                               const float* act_rstd, const float* act_w, const float* act_b, int act_gelu,
+                               const float* gate, int hw, float* dW, int accumulate, void* ws, int64_t ws_bytes,
+                               hipStream_t stream) {
+  if (nout <= 0 || nin <= 0 || rows <= 0) return 0;
+  if (ws_bytes < sm_linear_dw_se_workspace_bytes(rows, nout, nin)) return -4;
+  if (nout % 8 || nin % 8 || hw <= 0 || hw % BKT || rows % hw || (((uintptr_t)dy | (uintptr_t)a2) & 15)) return -2;
+  const int v = gemm_variant(nout, nin, rows);
+  if (v == 1) return -2;
+  GemmArgs g{};
+  g.M = nout; g.N = nin; g.K = rows; g.A = dy; g.lda = nout; g.B = a2; g.ldb = nin; g.C = dW; g.ldc = nin;
+  g.alpha = 1.f; g.beta = accumulate ? 1.f : 0.f; g.rows_per_group = 1;
+  g.xb_act = ChanAffine{act_mean, act_rstd, act_w, act_b, act_gelu};
+  g.xb_gate = gate; g.xb_hw = hw;
+  int splits = choose_splits(nout, nin, rows, true);
+  if (splits > 1) {
+    int chunk = (rows + splits - 1) / splits;
+    chunk = (chunk + BKT - 1) / BKT * BKT;     // K-steps never straddle a frame (hw % BKT == 0)
+    splits = (rows + chunk - 1) / chunk;
+    g.k_begin = 0; g.k_chunk = chunk; g.partial = (float*)ws;
+  } else {
+    g.k_begin = 0; g.k_chunk = rows;
+  }
+  const int bm = variant_bm(v);
+  const dim3 grid(((nin + 127) / 128) * ((nout + bm - 1) / bm) * splits);
+  if (v == 2) hipLaunchKernelGGL((gemm_bf16_v2<false, false, float, true, 256, 7>), grid, dim3(512), 0, stream, g);
+  else hipLaunchKernelGGL((gemm_bf16_v2<false, false, float, true, 128, 7>), grid, dim3(256), 0, stream, g);
+  SM_CHECK_LAUNCH();
+  if (splits > 1) {
+    const int64_t total = (int64_t)nout * nin;
+    int blocks = (int)((total + 255) / 256);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(splitk_reduce_kernel<float>, dim3(blocks), dim3(256), 0, stream, g, splits);
+    SM_CHECK_LAUNCH();
+  }
   return 0;
 }
 

@@ -240,12 +240,19 @@ class MBConvFn(torch.autograd.Function):
                        row_scale=st.dp_scale, rows_per_group=Ho * Wo)
         if ctx.fused:
             act2 = (m2, r2, g2.detach(), b2.detach(), True)
-            h3 = K.se_scale(a2, gate, Fr, Ho * Wo, mid, act=act2)
+            if (Ho * Wo) % 64 == 0:
+                # projection weight gradient with the SE output h3 formed in the GEMM's
+                # operand loads (no h3 round trip; bit-identical to se_scale + linear_dw)
+                K.linear_dw_se(da3, a2.view(-1, mid), act2, gate, Ho * Wo, G(w_proj).view(Cout, mid))
+            else:
+                h3 = K.se_scale(a2, gate, Fr, Ho * Wo, mid, act=act2)
+                K.linear_dw(da3, h3, G(w_proj).view(Cout, mid))
+                del h3
         else:
             h2 = K.bn_apply(a2, m2, r2, g2.detach(), b2.detach(), gelu=True)
             h3 = K.se_scale(h2, gate, Fr, Ho * Wo, mid)
-        K.linear_dw(da3, h3, G(w_proj).view(Cout, mid))
-        del h3
+            K.linear_dw(da3, h3, G(w_proj).view(Cout, mid))
+            del h3
         dh3 = K.linear_dx(da3, W(w_proj, mode).view(Cout, mid))
         del da3
         if ctx.fused:

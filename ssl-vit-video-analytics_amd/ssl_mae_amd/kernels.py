@@ -106,6 +106,22 @@ def linear_dw_bias(dy, x, grad_w, grad_b, gelu=None):
     return grad_w
 
 
+def linear_dw_se(dy, a2, act, gate, hw, grad_sink, accumulate=True):
+    """grad_sink[N,C] (+)= dy^T @ h3 with h3 = se_scale(a2, gate, act) formed in the GEMM's
+    operand loads (sm_linear_dw_se; bit-identical to se_scale + linear_dw).  dy [M,N],
+    a2 [M,C] bf16, gate [M/hw, C] fp32, hw % 64 == 0."""
+    _chk(dy, a2, gate, grad_sink)
+    M, N = dy.shape
+    C = a2.shape[1]
+    if a2.shape[0] != M or gate.shape != (M // hw, C) or M % hw or grad_sink.shape != (N, C):
+        raise _lib.KernelError("linear_dw_se: shape mismatch")
+    nbytes = query("sm_linear_dw_se_workspace_bytes", M, N, C)
+    ws = _ws(nbytes, dy.device)
+    call("sm_linear_dw_se", M, N, C, ptr(dy), ptr(a2), *_act_args(act), ptr(gate.contiguous()), int(hw),
+         ptr(grad_sink), 1 if accumulate else 0, ptr(ws), nbytes, stream())
+    return grad_sink
+
+
 def colsum(x, out, accumulate=True):
     M, C = x.shape
     nbytes = query("sm_colsum_workspace_bytes", M, C)

@@ -693,6 +693,21 @@ def se_scale(x, s, F, HW, C, act=None):
     return torch.ops.ssl_mae.se_scale(x, s, F, HW, C, *_act(act))
 
 
+@_op("linear_dw_se", "(Tensor dy, Tensor a2, Tensor act_mean, Tensor act_rstd, Tensor act_w, Tensor act_b, "
+                     "bool act_gelu, Tensor gate, int hw, Tensor(a!) grad_sink, bool accumulate) -> ()", ("grad_sink",))
+def _linear_dw_se(dy, a2, am, ar, aw, ab, ag, gate, hw, grad_sink, accumulate):
+    _K.linear_dw_se(dy, a2, (am, ar, aw, ab, ag), gate, hw, grad_sink, accumulate)
+
+
+_linear_dw_se.register_fake(_none)
+
+
+def linear_dw_se(dy, a2, act, gate, hw, grad_sink, accumulate=True):
+    """Weight gradient of the MBConv projection over the SE output, h3 formed on load."""
+    torch.ops.ssl_mae.linear_dw_se(dy, a2, *act[:4], bool(act[4]), gate, int(hw), grad_sink, bool(accumulate))
+    return grad_sink
+
+
 @_op("se_bwd", "(Tensor dy, Tensor x, int F, int HW, int C, Tensor w1, Tensor w2, Tensor s, Tensor h1, "
                "Tensor? act_mean, Tensor? act_rstd, Tensor? act_w, Tensor? act_b, bool act_gelu) "
                "-> (Tensor, Tensor, Tensor)")

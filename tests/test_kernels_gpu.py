@@ -706,6 +706,39 @@ def test_linear_dw_bias_gelu_operand(M, N, H, p):
     assert rel_err(gw2, ref) < 2e-2
 
 
+@pytest.mark.parametrize("Fr,HW,N,C,acc", [(3, 64, 96, 384, True), (5, 192, 96, 200, False), (2, 3136, 192, 768, True),
+                                           (64, 12544, 96, 384, True), (1, 128, 8, 8, False)])
+def test_linear_dw_se_operand(Fr, HW, N, C, acc):
+    """MBConv projection weight gradient over the SE output h3 = bf16(bf16(GELU(BN(a2)))
+    * gate) formed in the GEMM's B-operand loads (sm_linear_dw_se): bit-identical to
+    se_scale + linear_dw (the same split-K tiles and order), and the fp32 torch math of
+    the same bf16 h3.  Shapes: one-frame-per-K-step boundary (HW = 64), ragged channel
+    tile (C = 200: columns past N), split-K at the stage-1 / stage-0 step shapes
+    (Fr = 64 x 112^2 = 0.8 M rows), a single 8 x 8 tile."""
+    kk = KK()
+    M = Fr * HW
+    a2 = rnd(M, C, dtype=torch.bfloat16, seed=180, scale=2.0).to(DEV)
+    dy = rnd(M, N, dtype=torch.bfloat16, seed=181, scale=0.1).to(DEV)
+    mean = (torch.randn(C, generator=torch.Generator().manual_seed(182)) * 0.3).to(DEV)
+    rstd = (torch.rand(C, generator=torch.Generator().manual_seed(183)) + 0.5).to(DEV)
+    w = (torch.rand(C, generator=torch.Generator().manual_seed(184)) + 0.5).to(DEV)
+    b = (torch.randn(C, generator=torch.Generator().manual_seed(185)) * 0.1).to(DEV)
+    gate = torch.rand(Fr, C, generator=torch.Generator().manual_seed(186)).to(DEV)
+    act = (mean, rstd, w, b, True)
+    h3 = kk.se_scale(a2, gate, Fr, HW, C, act=act)
+    g1 = torch.full((N, C), 0.25, device=DEV)
+    g2 = g1.clone()
+    kk.linear_dw(dy, h3, g1, accumulate=acc)
+    kk.linear_dw_se(dy, a2, act, gate, HW, g2, accumulate=acc)
+    assert torch.equal(g1, g2)
+    ref = dy.float().t() @ h3.float() + (0.25 if acc else 0.0)
+    assert rel_err(g2, ref) < 1e-3
+    if Fr <= 5:   # h3 itself against fp32 torch math (bf16 roundings as the kernels)
+        hh = F.gelu((a2.float() * (rstd * w) + (b - mean * rstd * w))).to(torch.bfloat16).float()
+        hh = (hh.view(Fr, HW, C) * gate.view(Fr, 1, C)).view(M, C)
+        assert rel_err(h3.float(), hh) < 1e-2
+
+
 @pytest.mark.parametrize("Fr,H,C,s", [(4, 19, 64, 2), (4, 20, 64, 2), (3, 30, 32, 2), (2, 56, 768, 2),
                                       (4, 7, 1536, 2), (4, 4, 768, 2), (4, 8, 384, 2),
                                       (4, 19, 64, 1), (2, 112, 96, 1)])
