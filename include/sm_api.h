@@ -85,6 +85,16 @@ int sm_layernorm_bwd(int x_dtype, int dy_dtype, int dx_dtype, int64_t M, int C, 
                      const void* x, const float* mean, const float* rstd, const float* gamma,
                      void* dx, const void* dres, float* dgamma, float* dbeta, void* ws,
                      int64_t ws_bytes, hipStream_t st);
+/* sm_layernorm_bwd plus the block branch's copy of dx (C = 192 or 384): dxb [M][C] bf16 =
+ * bf16(bf16(dx) * row_scale[row / rows_per_group] * keep(row, col) / (1 - drop_p)) with
+ * sm_dropout_bwd's mask (row_scale may be null, drop_p 0): the cast / dropout-backward
+ * passes over dx that feed the branch's Linear backward (tiny_vit.py:126-128 DropPath,
+ * mae_vit_adapter.py:40-48 dropout1) folded into the LayerNorm backward; bit-identical. */
+int sm_layernorm_bwd_branch(int x_dtype, int dy_dtype, int dx_dtype, int64_t M, int C, const void* dy,
+                            const void* x, const float* mean, const float* rstd, const float* gamma, void* dx,
+                            const void* dres, float* dgamma, float* dbeta, void* dxb, float drop_p, uint64_t seed,
+                            const float* row_scale, int64_t rows_per_group, void* ws, int64_t ws_bytes,
+                            hipStream_t st);
 
 /* ---- BatchNorm2d, train mode (tiny_vit.py:16 Conv2d_BN), channels-last [M][C] */
 int64_t sm_bn_workspace_bytes(int64_t M, int C);
@@ -124,6 +134,11 @@ int sm_gelu_fwd(int dtype, int64_t n, int ncols, const void* x, void* y, float d
  * (nn.Dropout of the decoder layers; timm DropPath of tiny_vit.py:52,114) */
 int sm_dropout_bwd(int dtype, int64_t n, int ncols, const void* dy, void* dx, float drop_p, uint64_t seed,
                    const float* row_scale, int64_t rows_per_group, hipStream_t st);
+/* sm_cast (fp32 -> bf16) and sm_dropout_bwd in one pass: dx_bf16 = bf16(bf16(dy) *
+ * row_scale * keep / (1 - p)); the decoder block's fp32 residual-stream gradient entering
+ * its bf16 branch (torch.autocast's cast + nn.Dropout backward, mae_vit_adapter.py:40-48). */
+int sm_cast_dropout_bwd(int64_t n, int ncols, const float* dy, void* dx_bf16, float drop_p, uint64_t seed,
+                        const float* row_scale, int64_t rows_per_group, hipStream_t st);
 /* DropPath per-sample keep scales: out[i] = keep ? 1/(1-p) : 0 */
 int sm_droppath_scale(int n, float p, uint64_t seed, float* out, hipStream_t st);
 /* column sums (Linear bias gradients): out[c] (+)= sum_m x[m][c] */

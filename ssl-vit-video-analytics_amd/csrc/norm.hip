@@ -200,11 +200,24 @@ __global__ __launch_bounds__(256) void ln_fwd16_kernel(const TI* x, const float*
 }
 
 // dx (+ dres) and per-block partial dgamma / dbeta (part_g/part_b [block][C]).
+// Branch copy (bo != null): the transformer block's backward feeds dx to the residual
+// stream AND, through the branch regularisers' backward, to the branch's Linear:
+// bo = bf16(bf16(dx) * rs[row / rpg] * keep(row, col) / (1 - p)), i.e. the cast
+// (fp32 stream) and sm_dropout_bwd passes over dx folded into this one (same mask,
+// same roundings: bit-identical).
+struct LnBranch {
+  __bf16* bo;
+  float p;
+  uint64_t seed;
+  const float* rs;
+  int64_t rpg;
+};
+
 template <typename TI, typename TD, int C>
 __global__ __launch_bounds__(256) void ln_bwd16_kernel(const TD* dy, const TI* x, const float* mean,
                                                        const float* rstd, const float* g, TI* dx, float* part_g,
                                                        float* part_b, int64_t M, int64_t rows_per_block,
-                                                       const TI* dres) {
+                                                       const TI* dres, LnBranch br) {
   constexpr int U = C / 64;
   __shared__ float red[2][4][C];
   const int gl = threadIdx.x & 15, grp = threadIdx.x >> 4, w = threadIdx.x >> 6;
@@ -251,6 +264,21 @@ __global__ __launch_bounds__(256) void ln_bwd16_kernel(const TD* dy, const TI* x
         for (int j = 0; j < 4; ++j) o[j] += pr[j];
       }
       store4(dx + e0 + 64 * u, o);
+      if (br.bo) {
+        const float rsv = br.rs ? br.rs[row / br.rpg] : 1.f;
+        const float ks = br.p > 0.f ? 1.f / (1.f - br.p) : 1.f;
+        const uint32_t hsh = br.p > 0.f ? drop_hash(drop_rowbase(seed32(br.seed), (uint64_t)row),
+                                                     (uint32_t)(64 * u + 4 * gl)) : 0u;
+        const uint32_t thr = drop_thr(br.p);
+        float b4[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float d = (float)(__bf16)to_f<TI>(from_f<TI>(o[j]));   // the stored dx, cast to bf16
+          const float mj = br.p > 0.f ? (((hsh >> (8 * j)) & 0xFFu) >= thr ? ks : 0.f) : 1.f;
+          b4[j] = d * (rsv * mj);
+        }
+        store4(br.bo + e0 + 64 * u, b4);
+      }
     }
   }
   // column partials: the 4 row groups of a wave, then the 4 waves (fixed order)
@@ -539,14 +567,20 @@ __global__ void gelu_bwd_kernel(const T* pre, const TG* dy, TG* dx, int64_t tota
   }
 }
 
-// dx = dy * dropout_mask * row_scale[row / rpg]   (backward of the branch regularisers)
-template <typename T>
-__global__ void dropout_bwd_kernel(const T* dy, T* dx, int64_t total8, int ncols, float drop_p, uint64_t seed,
+// dx = dy * dropout_mask * row_scale[row / rpg]   (backward of the branch regularisers);
+// TO = bf16 < T = fp32: the autocast cast of the fp32 stream's gradient to the bf16
+// branch folded in (dy rounded to bf16 first, as the separate cast pass stores it)
+template <typename T, typename TO = T>
+__global__ void dropout_bwd_kernel(const T* dy, TO* dx, int64_t total8, int ncols, float drop_p, uint64_t seed,
                                    const float* row_scale, int64_t rpg) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total8;
        i += (int64_t)gridDim.x * blockDim.x) {
     float d[8], m[8];
     load8(dy + i * 8, d);
+    if (sizeof(TO) < sizeof(T)) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = to_f<TO>(from_f<TO>(d[j]));
+    }
     const int64_t e = i * 8;
     const float rs = row_scale ? row_scale[(e / ncols) / rpg] : 1.f;
     if (drop_p > 0.f) drop_mult8(e, ncols, drop_p, seed, m);
@@ -686,11 +720,35 @@ extern "C" int64_t sm_layernorm_bwd_workspace_bytes(int64_t M, int C) {
   return nb * C * 4 * 2;
 }
 
+static int layernorm_bwd(int x_dtype, int dy_dtype, int dx_dtype, int64_t M, int C, const void* dy, const void* x,
+                         const float* mean, const float* rstd, const float* gamma, void* dx, const void* dres,
+                         float* dgamma, float* dbeta, void* ws, int64_t ws_bytes, LnBranch br, hipStream_t st);
+
 // dx (+)= LN backward; dgamma/dbeta (+)= (accumulated into the fp32 grad sinks)
 extern "C" int sm_layernorm_bwd(int x_dtype, int dy_dtype, int dx_dtype, int64_t M, int C, const void* dy,
                                 const void* x, const float* mean, const float* rstd, const float* gamma,
                                 void* dx, const void* dres, float* dgamma, float* dbeta, void* ws,
                                 int64_t ws_bytes, hipStream_t st) {
+  return layernorm_bwd(x_dtype, dy_dtype, dx_dtype, M, C, dy, x, mean, rstd, gamma, dx, dres, dgamma, dbeta, ws,
+                       ws_bytes, LnBranch{nullptr, 0.f, 0, nullptr, 1}, st);
+}
+
+// sm_layernorm_bwd plus the branch copy dxb = bf16(bf16(dx) * row_scale[row / rpg] *
+// dropout keep / (1 - p)) (C = 192 or 384)
+extern "C" int sm_layernorm_bwd_branch(int x_dtype, int dy_dtype, int dx_dtype, int64_t M, int C, const void* dy,
+                                       const void* x, const float* mean, const float* rstd, const float* gamma,
+                                       void* dx, const void* dres, float* dgamma, float* dbeta, void* dxb,
+                                       float drop_p, uint64_t seed, const float* row_scale, int64_t rows_per_group,
+                                       void* ws, int64_t ws_bytes, hipStream_t st) {
+  if (C != 192 && C != 384) return -2;
+  if (dxb == nullptr || rows_per_group <= 0 || ((uintptr_t)dxb & 7)) return -2;
+  return layernorm_bwd(x_dtype, dy_dtype, dx_dtype, M, C, dy, x, mean, rstd, gamma, dx, dres, dgamma, dbeta, ws,
+                       ws_bytes, LnBranch{(__bf16*)dxb, drop_p, seed, row_scale, rows_per_group}, st);
+}
+
+static int layernorm_bwd(int x_dtype, int dy_dtype, int dx_dtype, int64_t M, int C, const void* dy, const void* x,
+                         const float* mean, const float* rstd, const float* gamma, void* dx, const void* dres,
+                         float* dgamma, float* dbeta, void* ws, int64_t ws_bytes, LnBranch br, hipStream_t st) {
   if (M <= 0) return 0;
   if (C % 4 || C > 1024) return -2;
   const int rpb = red_rows_per_block(M, C);
@@ -702,11 +760,11 @@ extern "C" int sm_layernorm_bwd(int x_dtype, int dy_dtype, int dx_dtype, int64_t
   if (C == 384)
     DISPATCH2(x_dtype, dy_dtype,
               hipLaunchKernelGGL((ln_bwd16_kernel<T1, T2, 384>), dim3(nb), dim3(256), 0, st, (const T2*)dy,
-                                 (const T1*)x, mean, rstd, gamma, (T1*)dx, pg, pb, M, (int64_t)rpb, (const T1*)dres));
+                                 (const T1*)x, mean, rstd, gamma, (T1*)dx, pg, pb, M, (int64_t)rpb, (const T1*)dres, br));
   else if (C == 192)
     DISPATCH2(x_dtype, dy_dtype,
               hipLaunchKernelGGL((ln_bwd16_kernel<T1, T2, 192>), dim3(nb), dim3(256), 0, st, (const T2*)dy,
-                                 (const T1*)x, mean, rstd, gamma, (T1*)dx, pg, pb, M, (int64_t)rpb, (const T1*)dres));
+                                 (const T1*)x, mean, rstd, gamma, (T1*)dx, pg, pb, M, (int64_t)rpb, (const T1*)dres, br));
   else
     DISPATCH2(x_dtype, dy_dtype,
               hipLaunchKernelGGL((ln_bwd_kernel<T1, T2, T1>), dim3(nb), dim3(256), 0, st, (const T2*)dy,
@@ -951,6 +1009,19 @@ extern "C" int sm_dropout_bwd(int dtype, int64_t n, int ncols, const void* dy, v
   else
     hipLaunchKernelGGL(dropout_bwd_kernel<float>, dim3(ew_blocks(n / 8)), dim3(256), 0, st, (const float*)dy,
                        (float*)dx, n / 8, ncols, drop_p, seed, row_scale, rpg);
+  SM_CHECK_LAUNCH();
+  return 0;
+}
+
+// cast fp32 -> bf16 and dropout backward in one pass (the decoder block's fp32 residual
+// gradient entering its bf16 branch): bit-identical to sm_cast + sm_dropout_bwd
+extern "C" int sm_cast_dropout_bwd(int64_t n, int ncols, const float* dy, void* dx_bf16, float drop_p, uint64_t seed,
+                                   const float* row_scale, int64_t rows_per_group, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (n % 8 || ncols % 8) return -2;
+  const int64_t rpg = rows_per_group > 0 ? rows_per_group : 1;
+  hipLaunchKernelGGL((dropout_bwd_kernel<float, __bf16>), dim3(ew_blocks(n / 8)), dim3(256), 0, st, dy,
+                     (__bf16*)dx_bf16, n / 8, ncols, drop_p, seed, row_scale, rpg);
   SM_CHECK_LAUNCH();
   return 0;
 }

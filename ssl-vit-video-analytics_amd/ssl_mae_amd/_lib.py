@@ -35,6 +35,9 @@ _SIGS = {
     "sm_layernorm_bwd_workspace_bytes": (_c_i64, [_c_i64, _c_i32]),
     "sm_layernorm_bwd": (_c_i32, [_c_i32, _c_i32, _c_i32, _c_i64, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p,
                                   _c_p, _c_p, _c_p, _c_p, _c_i64, _c_p]),
+    "sm_layernorm_bwd_branch": (_c_i32, [_c_i32, _c_i32, _c_i32, _c_i64, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p,
+                                         _c_p, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_u64, _c_p, _c_i64, _c_p, _c_i64,
+                                         _c_p]),
     "sm_bn_workspace_bytes": (_c_i64, [_c_i64, _c_i32]),
     "sm_bn_stats": (_c_i32, [_c_i32, _c_i64, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_f32, _c_f32, _c_i32,
                              _c_p, _c_i64, _c_p]),
@@ -44,6 +47,7 @@ _SIGS = {
                            _c_p, _c_p, _c_p, _c_p, _c_i64, _c_p]),
     "sm_gelu_bwd": (_c_i32, [_c_i32, _c_i32, _c_i64, _c_i32, _c_p, _c_p, _c_p, _c_f32, _c_u64, _c_p]),
     "sm_dropout_bwd": (_c_i32, [_c_i32, _c_i64, _c_i32, _c_p, _c_p, _c_f32, _c_u64, _c_p, _c_i64, _c_p]),
+    "sm_cast_dropout_bwd": (_c_i32, [_c_i64, _c_i32, _c_p, _c_p, _c_f32, _c_u64, _c_p, _c_i64, _c_p]),
     "sm_droppath_scale": (_c_i32, [_c_i32, _c_f32, _c_u64, _c_p, _c_p]),
     "sm_add": (_c_i32, [_c_i32, _c_i32, _c_i64, _c_p, _c_p, _c_p, _c_p]),
     "sm_cast": (_c_i32, [_c_i32, _c_i32, _c_i64, _c_p, _c_p, _c_p]),

@@ -335,9 +335,13 @@ class BlockFn(torch.autograd.Function):
         dout = dout.contiguous()
         if dout.dtype != x.dtype:
             dout = dout.to(x.dtype)
-        db = dout if dout.dtype == act else K.cast(dout, act)       # grad of the bf16 branch
-        if st.drop2 > 0 or st.dp2 is not None:
-            db = K.dropout_bwd(db, st.drop2, st.seed2, st.dp2, L)
+        regs2 = st.drop2 > 0 or st.dp2 is not None
+        if dout.dtype == torch.float32 and act == torch.bfloat16 and regs2:
+            db = K.cast_dropout_bwd(dout, st.drop2, st.seed2, st.dp2, L)   # cast + dropout in one pass
+        else:
+            db = dout if dout.dtype == act else K.cast(dout, act)       # grad of the bf16 branch
+            if regs2:
+                db = K.dropout_bwd(db, st.drop2, st.seed2, st.dp2, L)
         if rb:   # fc2 weight gradient of dropout(GELU(hpre)) (kernels.linear_dw_bias picks the form)
             K.linear_dw_bias(db, hpre, G(w2), G(b2), gelu=(st.drop_ff, st.seed_ff))
         else:
@@ -353,11 +357,20 @@ class BlockFn(torch.autograd.Function):
         del ln2
         dln2 = K.linear_dx(dhpre, W(w1, mode))
         del dhpre
-        dx2 = K.layernorm_bwd(dln2, x2, mu2, rs2, ln2w.detach(), G(ln2w), G(ln2b), dres=dout)
-        del dln2
-        dxb = dx2 if dx2.dtype == act else K.cast(dx2, act)
-        if st.drop1 > 0 or st.dp1 is not None:
-            dxb = K.dropout_bwd(dxb, st.drop1, st.seed1, st.dp1, L)
+        regs1 = st.drop1 > 0 or st.dp1 is not None
+        C = x2.shape[1]
+        if act == torch.bfloat16 and C in (192, 384) and (regs1 or x2.dtype != act):
+            # the branch's bf16 copy of dx (cast + dropout / DropPath backward) from the
+            # LayerNorm backward's own pass
+            dx2, dxb = K.layernorm_bwd_branch(dln2, x2, mu2, rs2, ln2w.detach(), G(ln2w), G(ln2b), dres=dout,
+                                              drop_p=st.drop1, seed=st.seed1, row_scale=st.dp1, rows_per_group=L)
+            del dln2
+        else:
+            dx2 = K.layernorm_bwd(dln2, x2, mu2, rs2, ln2w.detach(), G(ln2w), G(ln2b), dres=dout)
+            del dln2
+            dxb = dx2 if dx2.dtype == act else K.cast(dx2, act)
+            if regs1:
+                dxb = K.dropout_bwd(dxb, st.drop1, st.seed1, st.dp1, L)
         K.linear_dw_bias(dxb, o, G(wproj), G(bproj))
         do = K.linear_dx(dxb, W(wproj, mode))
         del dxb

@@ -175,6 +175,21 @@ def layernorm_bwd(dy, x, mean, rstd, gamma, dgamma, dbeta, dres=None):
     return dx
 
 
+def layernorm_bwd_branch(dy, x, mean, rstd, gamma, dgamma, dbeta, dres=None, drop_p=0.0, seed=0, row_scale=None,
+                         rows_per_group=1):
+    """layernorm_bwd plus the branch copy dxb = bf16(bf16(dx) * row_scale * dropout keep)
+    (sm_layernorm_bwd_branch; = cast + dropout_bwd of dx).  Returns (dx, dxb)."""
+    M, C = x.shape
+    dx = torch.empty_like(x)
+    dxb = torch.empty((M, C), dtype=torch.bfloat16, device=x.device)
+    nbytes = query("sm_layernorm_bwd_workspace_bytes", M, C)
+    ws = _ws(nbytes, x.device)
+    call("sm_layernorm_bwd_branch", dt(x), dt(dy), dt(dx), M, C, ptr(dy), ptr(x), ptr(mean), ptr(rstd), ptr(gamma),
+         ptr(dx), ptr(dres), ptr(dgamma), ptr(dbeta), ptr(dxb), float(drop_p), int(seed), ptr(row_scale),
+         int(rows_per_group), ptr(ws), nbytes, stream())
+    return dx, dxb
+
+
 # ------------------------------------------------------------------ BatchNorm (train)
 def bn_stats(x2d, running_mean=None, running_var=None, momentum=0.1, eps=1e-5, updates=1, num_batches=None):
     _chk(x2d)
@@ -241,6 +256,17 @@ def dropout_bwd(dy, drop_p=0.0, seed=0, row_scale=None, rows_per_group=1):
     dx = torch.empty_like(dy)
     call("sm_dropout_bwd", dt(dy), dy.numel(), dy.shape[-1], ptr(dy), ptr(dx), float(drop_p), int(seed),
          ptr(row_scale), int(rows_per_group), stream())
+    return dx
+
+
+def cast_dropout_bwd(dy, drop_p=0.0, seed=0, row_scale=None, rows_per_group=1):
+    """bf16(bf16(dy) * row_scale * dropout keep) of an fp32 dy in one pass (= cast + dropout_bwd)."""
+    _chk(dy)
+    if dy.dtype != torch.float32:
+        raise _lib.KernelError("cast_dropout_bwd takes an fp32 gradient")
+    dx = torch.empty(dy.shape, dtype=torch.bfloat16, device=dy.device)
+    call("sm_cast_dropout_bwd", dy.numel(), dy.shape[-1], ptr(dy), ptr(dx), float(drop_p), int(seed), ptr(row_scale),
+         int(rows_per_group), stream())
     return dx
 
 

@@ -279,6 +279,26 @@ def layernorm_bwd(dy, x, mean, rstd, gamma, dgamma, dbeta, dres=None):
     return torch.ops.ssl_mae.layernorm_bwd(dy, x, mean, rstd, gamma, dgamma, dbeta, dres)
 
 
+@_op("layernorm_bwd_branch", "(Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, Tensor(a!) dgamma, "
+                             "Tensor(b!) dbeta, Tensor? dres, float drop_p, int seed, Tensor? row_scale, "
+                             "int rows_per_group) -> (Tensor, Tensor)", ("dgamma", "dbeta"))
+def _layernorm_bwd_branch(dy, x, mean, rstd, gamma, dgamma, dbeta, dres, drop_p, seed, row_scale, rows_per_group):
+    return _K.layernorm_bwd_branch(dy, x, mean, rstd, gamma, dgamma, dbeta, dres, drop_p, _u64(seed), row_scale,
+                                   rows_per_group)
+
+
+_layernorm_bwd_branch.register_fake(
+    lambda dy, x, *a: (torch.empty_like(x), torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)))
+
+
+def layernorm_bwd_branch(dy, x, mean, rstd, gamma, dgamma, dbeta, dres=None, drop_p=0.0, seed=0, row_scale=None,
+                         rows_per_group=1):
+    """LayerNorm backward + the block branch's bf16 copy of dx with the branch's dropout /
+    DropPath backward applied (one pass over dx instead of three)."""
+    return torch.ops.ssl_mae.layernorm_bwd_branch(dy, x, mean, rstd, gamma, dgamma, dbeta, dres, float(drop_p),
+                                                  _s64(seed), row_scale, int(rows_per_group))
+
+
 # ============================================================================ BatchNorm
 @_op("bn_stats", "(Tensor x, Tensor(a!)? running_mean, Tensor(b!)? running_var, float momentum, float eps, "
                  "int updates, Tensor(c!)? num_batches_tracked) -> (Tensor, Tensor)",
@@ -391,6 +411,18 @@ _dropout_bwd.register_fake(lambda dy, *a: torch.empty_like(dy))
 
 def dropout_bwd(dy, drop_p=0.0, seed=0, row_scale=None, rows_per_group=1):
     return torch.ops.ssl_mae.dropout_bwd(dy, float(drop_p), _s64(seed), row_scale, int(rows_per_group))
+
+
+@_op("cast_dropout_bwd", "(Tensor dy, float drop_p, int seed, Tensor? row_scale, int rows_per_group) -> Tensor")
+def _cast_dropout_bwd(dy, drop_p, seed, row_scale, rows_per_group):
+    return _K.cast_dropout_bwd(dy, drop_p, _u64(seed), row_scale, rows_per_group)
+
+
+_cast_dropout_bwd.register_fake(lambda dy, *a: torch.empty(dy.shape, dtype=torch.bfloat16, device=dy.device))
+
+
+def cast_dropout_bwd(dy, drop_p=0.0, seed=0, row_scale=None, rows_per_group=1):
+    return torch.ops.ssl_mae.cast_dropout_bwd(dy, float(drop_p), _s64(seed), row_scale, int(rows_per_group))
 
 
 @_op("droppath_scale", "(int n, float p, int seed, Device device) -> Tensor")

@@ -44,7 +44,8 @@ def test_torch_library_registration():
     from ssl_mae_amd import _lib, ops
     registered = set(ops.registered_ops())
     alias = {"layernorm_fwd": "layernorm", "dwconv_fwd": "dwconv", "gelu_fwd": "gelu", "fill": "fill_",
-             "scale": "scale_", "dwconv_fused_fwd": "dwconv_fused", "pos_blend_fwd": "pos_blend"}
+             "scale": "scale_", "dwconv_fused_fwd": "dwconv_fused", "pos_blend_fwd": "pos_blend",
+             "dwconv_s2_bn_bwd": "dwconv_bn_bwd"}   # ssl_mae::dwconv_bn_bwd dispatches on stride
     internal = {"add",                       # not used by the step
                 "bn_stats_from_partials"}    # the statistics step inside ssl_mae::dwconv_fused
     for sym in _lib.exported_symbols():

@@ -238,6 +238,38 @@ def test_layernorm(xd, yd, C):
     assert rel_err(db, br.grad) < 1e-4
 
 
+@pytest.mark.parametrize("xd,p,rs,C", [(torch.float32, 0.1, False, 384), (torch.float32, 0.0, False, 384),
+                                       (torch.bfloat16, 0.0, True, 384), (torch.bfloat16, 0.0, True, 192),
+                                       (torch.float32, 0.1, True, 192), (torch.bfloat16, 0.1, False, 384)])
+def test_layernorm_bwd_branch(xd, p, rs, C):
+    """LayerNorm backward with the block branch's bf16 copy of dx (sm_layernorm_bwd_branch):
+    dx and the weight gradients bit-identical to sm_layernorm_bwd, the copy bit-identical
+    to cast + dropout_bwd (dropout mask, DropPath row scale per group of rows); and the
+    fused fp32 -> bf16 cast + dropout backward (sm_cast_dropout_bwd) bit-identical to the
+    two passes."""
+    kk = KK()
+    M, L = 777, 37
+    x = ((rnd(M, C, seed=45) * 3 + 1).to(xd)).to(DEV)
+    g = (rnd(C, seed=46) * 0.1 + 1).to(DEV)
+    b = (rnd(C, seed=47) * 0.1).to(DEV)
+    dy = rnd(M, C, seed=48).to(torch.bfloat16).to(DEV)
+    res = rnd(M, C, seed=49).to(xd).to(DEV)
+    _, mean, rstd = kk.layernorm(x, g, b, out_dtype=torch.bfloat16)
+    row_scale = kk.droppath_scale((M + L - 1) // L, 0.2, 1234, DEV) if rs else None
+    dg1, db1 = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    dg2, db2 = dg1.clone(), db1.clone()
+    dx1 = kk.layernorm_bwd(dy, x, mean, rstd, g, dg1, db1, dres=res)
+    ref = dx1 if xd == torch.bfloat16 else kk.cast(dx1, torch.bfloat16)
+    ref = kk.dropout_bwd(ref, p, 99, row_scale, L)
+    dx2, dxb = kk.layernorm_bwd_branch(dy, x, mean, rstd, g, dg2, db2, dres=res, drop_p=p, seed=99,
+                                       row_scale=row_scale, rows_per_group=L)
+    assert torch.equal(dx1, dx2) and torch.equal(dg1, dg2) and torch.equal(db1, db2)
+    assert dxb.dtype == torch.bfloat16 and torch.equal(dxb, ref)
+    if xd == torch.float32:
+        fused = kk.cast_dropout_bwd(dx1, p, 99, row_scale, L)
+        assert torch.equal(fused, ref)
+
+
 # ------------------------------------------------------------------ BatchNorm
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("C", [48, 96, 384, 768])
