@@ -139,6 +139,16 @@ def dwse(args):
         t1 = timeit(lambda: K.linear_dw_se(dy, a2, act, gate, HW, g2, accumulate=False), args.iters)
         print(f"{name}: rows={M} dW[{N}][{C}]  se_scale + dW {t0:7.3f} ms | dW(se operand) {t1:7.3f} ms | "
               f"bit-identical {same}", flush=True)
+        if HW % 128 == 0:   # forward: se_fwd's h3 + linear against linear_se
+            w = (torch.randn(N, C, device=dev) * 0.1).to(torch.bfloat16)
+            w1 = torch.randn(C // 4, C, device=dev) * 0.1
+            w2 = torch.randn(C, C // 4, device=dev) * 0.1
+            t2 = timeit(lambda: K.linear(K.se_fwd(a2, Fn, HW, C, w1, w2, act=act)[0], w), args.iters)
+            t3 = timeit(lambda: K.linear_se(a2, w, act, K.se_fwd(a2, Fn, HW, C, w1, w2, act=act, want_y=False)[3],
+                                            HW), args.iters)
+            t4 = timeit(lambda: K.se_fwd(a2, Fn, HW, C, w1, w2, act=act, want_y=False), args.iters)
+            print(f"{name} fwd: se_fwd + proj {t2:7.3f} ms | se gate + proj(se operand) {t3:7.3f} ms "
+                  f"(se gate alone {t4:7.3f} ms)", flush=True)
         del a2, dy
         torch.cuda.empty_cache()
 

@@ -50,8 +50,8 @@ struct GemmArgs {
   // weight-gradient B operand formed on load (XformColsB): IMP 5 dropout after the GELU
   float xb_p;
   uint64_t xb_seed;
-  // IMP 7: the SE output act(x) * gate[frame][n] with act = the BatchNorm + GELU of the
-  // stored pre-activation (ChanAffine) and xb_hw token rows per frame
+  // IMP 7 (B) / IMP 6 (A): the SE output act(x) * gate[frame][channel] with act = the
+  // BatchNorm + GELU of the stored pre-activation (ChanAffine), xb_hw token rows per frame
   ChanAffine xb_act;
   const float* xb_gate;
   int xb_hw;
@@ -435,6 +435,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
 // pointer updates and zero-fill moves), which frees the registers for 4 waves per
 // SIMD at BM = 256.
 constexpr uint32_t BUF_OOB = 0x40000000u;   // >= num_records: the load returns 0
+constexpr int XA_MAXK = 1536;                // IMP 6: channels of the transformed A operand
 
 template <int ROWS>
 SM_DEV int mnmaj_off_r(int krow, int col) {   // [64][ROWS] MN-major tile (ROWS*2-B rows)
@@ -703,17 +704,20 @@ struct XformColsB {
 };
 
 // IMP: 0 plain operands; 1 A is the implicit im2col of a conv (ConvRowsA);
-// 2 B is (ConvColsB); 5 / 7 B is formed on load (XformColsB).
+// 2 B is (ConvColsB); 5 / 7 B is formed on load (XformColsB); 6 A (K-major) is the
+// SE output formed on load (below).
 // (IMP 5: the activation's registers do not fit beside the staging set at 4 waves /
 // SIMD -- scratch spills inside the K loop -- so it runs at 2 waves / SIMD.)
 template <bool AK, bool BK, typename TC, bool VEC, int BMV, int IMP = 0>
-__global__ __launch_bounds__(BMV * 2, (BMV == 256 && IMP != 5 && IMP != 7) ? 4 : 2) void gemm_bf16_v2(GemmArgs g) {
+__global__ __launch_bounds__(BMV * 2, (BMV == 256 && IMP != 5 && IMP != 6 && IMP != 7) ? 4 : 2) void gemm_bf16_v2(GemmArgs g) {
   constexpr int NT = BMV * 2, BNV = 128;
   constexpr bool XB = IMP == 5 || IMP == 7;
   constexpr int LDS_MAIN = (BMV + BNV) * BKT * 2, LDS_EPI = (NT / 64) * 8192;   // operand tiles | row stage
   __shared__ __attribute__((aligned(16))) char lds[LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI];
   char* la = lds;
   char* lb = lds + BMV * BKT * 2;
+  // IMP 6: per-channel table of the A transform (BN scale, shift, SE gate of the tile's frame)
+  __shared__ __attribute__((aligned(16))) float xtab[IMP == 6 ? 3 * XA_MAXK : 4];
   // 1-D grid over (split zs, tile), split-major, with the bijective XCD remap: the
   // n-tiles of one m-tile (sharing the A panel) and, under split-K, all tiles of one
   // split (sharing its token rows of both operands) are dealt to one XCD's L2.
@@ -731,6 +735,16 @@ __global__ __launch_bounds__(BMV * 2, (BMV == 256 && IMP != 5 && IMP != 7) ? 4 :
   const __bf16* B = (const __bf16*)g.B;
   const int kb = g.k_begin + zs * g.k_chunk;
   const int ke = min(g.K, kb + g.k_chunk);
+  if constexpr (IMP == 6) {   // the tile's rows lie in one frame (host: xb_hw % BMV == 0)
+    const int64_t frame = (int64_t)m0 / g.xb_hw;
+    for (int c = threadIdx.x; c < g.K; c += NT) {
+      const float sc = g.xb_act.rstd[c] * g.xb_act.w[c];   // = Affine8::init
+      xtab[c] = sc;
+      xtab[XA_MAXK + c] = g.xb_act.b[c] - g.xb_act.mean[c] * sc;
+      xtab[2 * XA_MAXK + c] = g.xb_gate[frame * g.K + c];
+    }
+    __syncthreads();
+  }
 
   TileLoader<BMV, NT, AK> tla;
   TileLoader<BNV, NT, BK> tlb;
@@ -789,8 +803,31 @@ __global__ __launch_bounds__(BMV * 2, (BMV == 256 && IMP != 5 && IMP != 7) ? 4 :
         for (int j = 0; j < 8; ++j) cs8[j] += (float)v[j];
       }
     }
-    if constexpr (IMP == 1) cla.store(la, ra);
-    else tla.store(la, ra);
+    if constexpr (IMP == 1) {
+      cla.store(la, ra);
+    } else if constexpr (IMP == 6) {
+      // h3 = bf16(bf16(GELU(a2 sc + sh)) * gate), exactly as se_apply_kernel stores it;
+      // the thread's 8 channels are fixed per K-step (k0 + kk0 ..)
+      const int c0 = k0 + tla.kk0;
+      float sc[8], sh[8], gt[8];
+      load8(xtab + c0, sc);
+      load8(xtab + XA_MAXK + c0, sh);
+      load8(xtab + 2 * XA_MAXK + c0, gt);
+#pragma unroll
+      for (int i = 0; i < TileLoader<BMV, NT, AK>::CH; ++i) {
+        float v[8];
+        load8((const __bf16*)&ra[i], v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float t = v[j] * sc[j] + sh[j];
+          v[j] = to_f<__bf16>(from_f<__bf16>(g.xb_act.gelu ? gelu_f(t) : t)) * gt[j];
+        }
+        ra[i] = pack8(v, (__bf16*)nullptr);
+      }
+      tla.store(la, ra);
+    } else {
+      tla.store(la, ra);
+    }
     if constexpr (IMP == 2) clb.store(lb, rb);
     else if constexpr (XB) xlb.store(lb, g, n0, k0);
     else tlb.store(lb, rb);
@@ -974,8 +1011,12 @@ int gemm_variant(int M, int N, int K) {
     return (x >= 1 && x <= 3) ? x : 0;
   }();
   if (forced) return forced;
+  // 384-row weight gradients with narrow rows (dW [384][384], [384][96]): three full
+  // 128-row tiles instead of two 256-row tiles, one a quarter empty -- measured
+  // 0.86 -> 0.79 ms and 5.18 -> 4.45 ms; wider (N = 1536) and 192-row ones are faster at
+  // BM = 256 (profiles/r02q/dw_bm_ab.txt)
+  if (M == 384 && N <= 384) return 3;
   return M >= 192 ? 2 : 3;
-  (void)N;
   (void)K;
 }
 int variant_bm(int v) { return v == 2 ? 256 : 128; }
@@ -1224,6 +1265,29 @@ extern "C" int sm_linear_dw_bias_gelu(int rows, int nout, int nin, const void* d
 // gate[r / hw][c]) formed in the B-operand loads (IMP 7): se_scale's h3 pass (read a2,
 // write h3, read it back) disappears.  a2 [rows][nin] bf16, dy [rows][nout] bf16;
 // rows = frames * hw with hw % 64 == 0 (each 64-row K-step inside one frame).
+// The MBConv projection's forward over the SE output (tiny_vit.py:29-34, 53): y[rows][nout]
+// (bf16) = h3 W^T with h3[r][c] = bf16(bf16(act(a2[r][c])) * gate[r / hw][c]) formed in the
+// A-operand loads (IMP 6): se_apply's h3 pass (read a2, write h3, read it back) is gone;
+// bit-identical to sm_se_fwd's h3 + sm_gemm.  hw % 128 == 0 (a tile inside one frame),
+// nin % 64 == 0, nin <= 1536.
+extern "C" int sm_linear_se(int rows, int nout, int nin, const void* a2, const void* w, const float* act_mean,
+                            const float* act_rstd, const float* act_w, const float* act_b, int act_gelu,
+                            const float* gate, int hw, void* y, hipStream_t stream) {
+  if (rows <= 0 || nout <= 0) return 0;
+  if (nin <= 0 || nin % BKT || nin > XA_MAXK || nout % 8 || hw <= 0 || hw % 128 || rows % hw ||
+      act_mean == nullptr || (((uintptr_t)a2 | (uintptr_t)w | (uintptr_t)y) & 15))
+    return -2;
+  GemmArgs g{};
+  g.M = rows; g.N = nout; g.K = nin; g.A = a2; g.lda = nin; g.B = w; g.ldb = nin; g.C = y; g.ldc = nout;
+  g.alpha = 1.f; g.beta = 0.f; g.rows_per_group = 1; g.k_begin = 0; g.k_chunk = nin;
+  g.xb_act = ChanAffine{act_mean, act_rstd, act_w, act_b, act_gelu};
+  g.xb_gate = gate; g.xb_hw = hw;
+  const dim3 grid(((nout + 127) / 128) * ((rows + 127) / 128));
+  hipLaunchKernelGGL((gemm_bf16_v2<true, true, __bf16, true, 128, 6>), grid, dim3(256), 0, stream, g);
+  SM_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int64_t sm_linear_dw_se_workspace_bytes(int rows, int nout, int nin) {
   const int s = choose_splits(nout, nin, rows, true);
   return s > 1 ? (int64_t)s * nout * nin * 4 : 16;

@@ -194,7 +194,13 @@ class MBConvFn(torch.autograd.Function):
                 a2 = K.dwconv_fused(a1, act0, w_dw.detach().view(mid, 9), Fr, H, Wd, mid, s)
                 m2, r2 = K.bn_eval_params(st.bn2)
             act2 = (m2, r2, g2.detach(), b2.detach(), True)
-            h3, pooled, h1se, gate = K.se_fwd(a2, Fr, Ho * Wo, mid, w_fc0.detach(), w_fc2.detach(), act=act2)
+            if (Ho * Wo) % 128 == 0 and mid % 64 == 0 and mid <= 1536:
+                # SE gate only; the projection GEMM forms h3 = act(a2) * gate in its operand
+                # loads (no h3 round trip; bit-identical to se_fwd's h3 + linear)
+                pooled, h1se, gate = K.se_gate(a2, Fr, Ho * Wo, mid, w_fc0.detach(), w_fc2.detach(), act=act2)
+                h3 = None
+            else:
+                h3, pooled, h1se, gate = K.se_fwd(a2, Fr, Ho * Wo, mid, w_fc0.detach(), w_fc2.detach(), act=act2)
         else:
             h1, m0, r0 = _bn_forward(a1, st.bn0, gelu=True, updates=st.bn_updates)
             a2 = K.dwconv(h1, w_dw.detach().view(mid, 9), Fr, H, Wd, mid, s)
@@ -202,7 +208,10 @@ class MBConvFn(torch.autograd.Function):
             h2, m2, r2 = _bn_forward(a2, st.bn2, gelu=True, updates=st.bn_updates)
             h3, pooled, h1se, gate = K.se_fwd(h2, Fr, Ho * Wo, mid, w_fc0.detach(), w_fc2.detach())
             del h2
-        a3 = K.linear(h3, W(w_proj, mode).view(Cout, mid))
+        if h3 is None:
+            a3 = K.linear_se(a2.view(-1, mid), W(w_proj, mode).view(Cout, mid), act2, gate, Ho * Wo)
+        else:
+            a3 = K.linear(h3, W(w_proj, mode).view(Cout, mid))
         del h3
         mean5, rstd5 = _bn_params(a3, st.bn5, st.bn_updates)
         out = K.bn_apply(a3, mean5, rstd5, g5.detach(), b5.detach(), residual=x2d if st.res else None,

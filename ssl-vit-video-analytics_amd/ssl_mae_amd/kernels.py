@@ -106,6 +106,21 @@ def linear_dw_bias(dy, x, grad_w, grad_b, gelu=None):
     return grad_w
 
 
+def linear_se(a2, w, act, gate, hw):
+    """y [M,N] bf16 = h3 @ w^T with h3 = se_scale(a2, gate, act) formed in the GEMM's
+    A-operand loads (sm_linear_se; bit-identical to se_fwd's h3 + linear).  a2 [M,C] bf16,
+    w [N,C] bf16, gate [M/hw, C] fp32, hw % 128 == 0, C % 64 == 0."""
+    _chk(a2, w, gate)
+    M, C = a2.shape
+    N = w.shape[0]
+    if w.shape[1] != C or gate.shape != (M // hw, C) or M % hw:
+        raise _lib.KernelError("linear_se: shape mismatch")
+    y = torch.empty((M, N), dtype=torch.bfloat16, device=a2.device)
+    call("sm_linear_se", M, N, C, ptr(a2), ptr(w), *_act_args(act), ptr(gate.contiguous()), int(hw), ptr(y),
+         stream())
+    return y
+
+
 def linear_dw_se(dy, a2, act, gate, hw, grad_sink, accumulate=True):
     """grad_sink[N,C] (+)= dy^T @ h3 with h3 = se_scale(a2, gate, act) formed in the GEMM's
     operand loads (sm_linear_dw_se; bit-identical to se_scale + linear_dw).  dy [M,N],

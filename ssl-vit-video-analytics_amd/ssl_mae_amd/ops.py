@@ -711,6 +711,26 @@ def se_fwd(x, F, HW, C, w1, w2, act=None):
     return torch.ops.ssl_mae.se_fwd(x, F, HW, C, w1, w2, *_act(act))
 
 
+@_op("se_gate", "(Tensor x, int F, int HW, int C, Tensor w1, Tensor w2, Tensor? act_mean, Tensor? act_rstd, "
+                "Tensor? act_w, Tensor? act_b, bool act_gelu) -> (Tensor, Tensor, Tensor)")
+def _se_gate(x, F, HW, C, w1, w2, am, ar, aw, ab, ag):
+    act = None if am is None else (am, ar, aw, ab, ag)
+    return _K.se_fwd(x, F, HW, C, w1, w2, act=act, want_y=False)[1:]
+
+
+@_se_gate.register_fake
+def _(x, F, HW, C, w1, w2, *a):
+    R = w1.shape[0]
+    f = torch.float32
+    return x.new_empty((F, C), dtype=f), x.new_empty((F, R), dtype=f), x.new_empty((F, C), dtype=f)
+
+
+def se_gate(x, F, HW, C, w1, w2, act=None):
+    """SELayer's pooled / hidden / gate without the scaled output (sm_se_fwd, y = null):
+    the consumer forms act(x) * gate in its own loads (linear_se)."""
+    return torch.ops.ssl_mae.se_gate(x, F, HW, C, w1, w2, *_act(act))
+
+
 @_op("se_scale", "(Tensor x, Tensor s, int F, int HW, int C, Tensor? act_mean, Tensor? act_rstd, Tensor? act_w, "
                  "Tensor? act_b, bool act_gelu) -> Tensor")
 def _se_scale(x, s, F, HW, C, am, ar, aw, ab, ag):
@@ -723,6 +743,20 @@ _se_scale.register_fake(lambda x, *a: torch.empty_like(x))
 
 def se_scale(x, s, F, HW, C, act=None):
     return torch.ops.ssl_mae.se_scale(x, s, F, HW, C, *_act(act))
+
+
+@_op("linear_se", "(Tensor a2, Tensor w, Tensor act_mean, Tensor act_rstd, Tensor act_w, Tensor act_b, "
+                  "bool act_gelu, Tensor gate, int hw) -> Tensor")
+def _linear_se(a2, w, am, ar, aw, ab, ag, gate, hw):
+    return _K.linear_se(a2, w, (am, ar, aw, ab, ag), gate, hw)
+
+
+_linear_se.register_fake(lambda a2, w, *a: a2.new_empty((a2.shape[0], w.shape[0]), dtype=torch.bfloat16))
+
+
+def linear_se(a2, w, act, gate, hw):
+    """Forward of the MBConv projection over the SE output, h3 formed on load."""
+    return torch.ops.ssl_mae.linear_se(a2, w, *act[:4], bool(act[4]), gate, int(hw))
 
 
 @_op("linear_dw_se", "(Tensor dy, Tensor a2, Tensor act_mean, Tensor act_rstd, Tensor act_w, Tensor act_b, "

@@ -771,6 +771,35 @@ def test_linear_dw_se_operand(Fr, HW, N, C, acc):
         assert rel_err(h3.float(), hh) < 1e-2
 
 
+@pytest.mark.parametrize("Fr,HW,N,C", [(3, 128, 96, 384), (2, 256, 192, 768), (16, 12544, 96, 384),
+                                       (5, 384, 40, 64), (1, 128, 8, 1536)])
+def test_linear_se_operand(Fr, HW, N, C):
+    """MBConv projection forward over the SE output with h3 = bf16(bf16(GELU(BN(a2))) *
+    gate) formed in the GEMM's A-operand loads (sm_linear_se): bit-identical to se_fwd's
+    h3 + linear, and the gate-only SE call (se_fwd, y = null) returns the same pooled /
+    hidden / gate.  Shapes: tiles of one frame at HW = 128, the stage-0 frame (112^2),
+    a ragged output width (N = 40: columns past N), K = 64 and K = 1536 (the table bound)."""
+    kk = KK()
+    M = Fr * HW
+    a2 = rnd(M, C, dtype=torch.bfloat16, seed=190, scale=2.0).to(DEV)
+    w = rnd(N, C, dtype=torch.bfloat16, seed=191, scale=0.1).to(DEV)
+    mean = (torch.randn(C, generator=torch.Generator().manual_seed(192)) * 0.3).to(DEV)
+    rstd = (torch.rand(C, generator=torch.Generator().manual_seed(193)) + 0.5).to(DEV)
+    gw = (torch.rand(C, generator=torch.Generator().manual_seed(194)) + 0.5).to(DEV)
+    gb = (torch.randn(C, generator=torch.Generator().manual_seed(195)) * 0.1).to(DEV)
+    act = (mean, rstd, gw, gb, True)
+    R = C // 4
+    w1 = rnd(R, C, seed=196, scale=0.1).to(DEV)
+    w2 = rnd(C, R, seed=197, scale=0.1).to(DEV)
+    h3, pooled, h1, gate = kk.se_fwd(a2, Fr, HW, C, w1, w2, act=act)
+    y_none, pooled2, h12, gate2 = kk.se_fwd(a2, Fr, HW, C, w1, w2, act=act, want_y=False)
+    assert y_none is None and torch.equal(pooled, pooled2) and torch.equal(h1, h12) and torch.equal(gate, gate2)
+    ref = kk.linear(h3, w)
+    y = kk.linear_se(a2, w, act, gate, HW)
+    assert y.dtype == torch.bfloat16 and torch.equal(y, ref)
+    assert rel_err(y.float(), h3.float() @ w.float().t()) < 1e-2
+
+
 @pytest.mark.parametrize("Fr,H,C,s", [(4, 19, 64, 2), (4, 20, 64, 2), (3, 30, 32, 2), (2, 56, 768, 2),
                                       (4, 7, 1536, 2), (4, 4, 768, 2), (4, 8, 384, 2),
                                       (4, 19, 64, 1), (2, 112, 96, 1)])
