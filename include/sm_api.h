@@ -56,6 +56,22 @@ int sm_linear_dw_bias(int rows, int nout, int nin, const void* dy, const void* x
 int sm_linear_dw_bias_gelu(int rows, int nout, int nin, const void* dy, const void* pre, float drop_p,
                            uint64_t seed, float* dW, float* db, int accumulate, void* ws, int64_t ws_bytes,
                            hipStream_t stream);
+/* y = x W^T (bf16, no bias) plus the train-mode BatchNorm statistics of y (Conv2d_BN,
+ * tiny_vit.py:12-18, of the MBConv expand conv tiny_vit.py:43): the GEMM epilogue sums the
+ * stored values per 64-row slab; fixed-order fp64 reduction, mean / rstd and the running
+ * statistics update (`updates` times) as sm_bn_stats -- replaces sm_gemm + sm_bn_stats
+ * (one read pass of y fewer).  x [M][K], w [N][K] bf16. */
+int64_t sm_linear_bn_stats_workspace_bytes(int M, int N);
+int sm_linear_bn_stats(int M, int N, int K, const void* x, const void* w, void* y, float* mean, float* rstd,
+                       float* run_mean, float* run_var, int64_t* num_batches_tracked, float momentum, float eps,
+                       int updates, void* ws, int64_t ws_bytes, hipStream_t stream);
+/* The MBConv projection's forward over the SE output (tiny_vit.py:29-34, 53): y[rows][nout]
+ * bf16 = h3 W^T, h3 = bf16(bf16(act(a2)) * gate[r / hw][c]) formed in the GEMM's operand
+ * loads exactly as sm_se_fwd stores it (bit-identical to sm_se_fwd's y + sm_gemm), w
+ * [nout][nin] bf16; hw % 128 == 0, nin % 64 == 0, nin <= 1536. */
+int sm_linear_se(int rows, int nout, int nin, const void* a2, const void* w, const float* act_mean,
+                 const float* act_rstd, const float* act_w, const float* act_b, int act_gelu, const float* gate,
+                 int hw, void* y, hipStream_t stream);
 /* The MBConv projection's weight gradient over the SE output (tiny_vit.py:29-34, 53,
  * replacing the Conv2d weight-gradient autograd node fed by SELayer.forward's product):
  * dW[nout][nin] (+)= dy^T h3, h3[r][c] = bf16(bf16(act(a2[r][c])) * gate[r / hw][c]),

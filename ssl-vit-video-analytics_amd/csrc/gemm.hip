@@ -55,6 +55,9 @@ struct GemmArgs {
   ChanAffine xb_act;
   const float* xb_gate;
   int xb_hw;
+  // BatchNorm statistics of the bf16 output (sm_linear_bn_stats): per-wave column sums
+  // and sums of squares of the stored values, [m-tile x waves along M][2][N]
+  float* stat_part;
 };
 
 template <typename TC>
@@ -157,18 +160,50 @@ struct RowStage {
   }
   // rows: tile rows [row0, row0 + 32) of out (ld elements) at column col0; 16-B chunk
   // c holds `cpc` columns; rows >= M or chunk columns >= N are not stored
-  template <typename TC>
-  SM_DEV void flush(int region, TC* out, int64_t ld, int64_t row0, int col0, int M, int N, int l) const {
+  // st1 / st2 (bf16 images): column sums / sums of squares of the stored rows of this
+  // 32-row image accumulated into lanes 0..7 (chunk l = 8 columns), for BatchNorm
+  // statistics of the output
+  template <typename TC, bool STATS = false>
+  SM_DEV void flush(int region, TC* out, int64_t ld, int64_t row0, int col0, int M, int N, int l,
+                    float* st1 = nullptr, float* st2 = nullptr) const {
     constexpr int cpc = 16 / sizeof(TC);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const int c = l & 7;
+    float a1[8], a2[8];
+    if constexpr (STATS) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a1[e] = a2[e] = 0.f;
+    }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int r = (l >> 3) + 8 * q;
       const uint4 v = *(const uint4*)(base + region * 4096 + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
       const int64_t row = row0 + r;
       const int col = col0 + c * cpc;
-      if (row < M && col < N) *(uint4*)(out + row * ld + col) = v;
+      if (row < M && col < N) {
+        *(uint4*)(out + row * ld + col) = v;
+        if constexpr (STATS) {
+          const bf16x8 b = __builtin_bit_cast(bf16x8, v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float f = (float)b[e];
+            a1[e] += f;
+            a2[e] = fmaf(f, f, a2[e]);
+          }
+        }
+      }
+    }
+    if constexpr (STATS) {   // the 8 row groups (l >> 3) of each chunk, fixed order
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+#pragma unroll
+        for (int x = 8; x < 64; x <<= 1) {
+          a1[e] += __shfl_xor(a1[e], x, 64);
+          a2[e] += __shfl_xor(a2[e], x, 64);
+        }
+        st1[e] += a1[e];
+        st2[e] += a2[e];
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
@@ -260,6 +295,9 @@ SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x
     return;
   }
   const RowStage rs_{stage};
+  float st1[8], st2[8];   // output statistics (g.stat_part, bf16 staged path)
+#pragma unroll
+  for (int e = 0; e < 8; ++e) st1[e] = st2[e] = 0.f;
   const bool bias_vec = g.bias && ((uintptr_t)g.bias & 15) == 0;
   const bool has_r = g.beta != 0.f;
   const TC* Rsrc = g.R ? (const TC*)g.R : (const TC*)g.C;
@@ -356,7 +394,20 @@ SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x
       const int64_t r0 = m0 + wm + 32 * i;
       const int c0 = n0 + wn;
       if (g.aux && (g.epi & 1)) rs_.flush<TC>(1, (TC*)g.aux, g.ldc, r0, c0, g.M, g.N, l);
-      rs_.flush<TC>(0, (TC*)g.C, g.ldc, r0, c0, g.M, g.N, l);
+      if (g.stat_part) rs_.flush<TC, true>(0, (TC*)g.C, g.ldc, r0, c0, g.M, g.N, l, st1, st2);
+      else rs_.flush<TC>(0, (TC*)g.C, g.ldc, r0, c0, g.M, g.N, l);
+    }
+  }
+  if (stage && sizeof(TC) == 2 && g.stat_part && l < 8 && m0 + wm < g.M) {   // this wave's 64 rows x 64 cols
+    const int wrow = (m0 + wm) >> 6;                         // part row = 64-row slab of the output
+    const int col = n0 + wn + 8 * l;
+    if (col < g.N) {
+      float* ps = g.stat_part + (int64_t)wrow * 2 * g.N + col;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        ps[e] = st1[e];
+        ps[g.N + e] = st2[e];
+      }
     }
   }
 }
@@ -1286,6 +1337,69 @@ extern "C" int sm_linear_se(int rows, int nout, int nin, const void* a2, const v
   hipLaunchKernelGGL((gemm_bf16_v2<true, true, __bf16, true, 128, 6>), grid, dim3(256), 0, stream, g);
   SM_CHECK_LAUNCH();
   return 0;
+}
+
+// y = x W^T (bf16 out, nn.Linear / 1x1 conv without bias) plus the train-mode BatchNorm
+// statistics of y (tiny_vit.py:16, the BN of the MBConv expand conv, :43): the GEMM epilogue
+// sums the stored bf16 values per 64-row slab and column (part [M / 64][2][N]), then the
+// fixed-order fp64 reduction + finalize / running-stat update of sm_bn_stats_from_partials
+// -- no separate statistics pass over y.  x [M][K], w [N][K] bf16, N % 8 == 0.
+constexpr int LBS_CHUNKS = 512;   // first-level row chunks of the slab partials
+
+// part[nb][ncols] -> out[chunk][ncols]: fixed-order fp64 sums of row chunks (chunk =
+// blockIdx.y), rounded to fp32 -- a many-block first level ahead of the 24-block colred
+// (hundreds of thousands of 64-row slabs at the stage-0 shape)
+__global__ __launch_bounds__(256) void rowchunk_sum_kernel(const float* part, int64_t nb, int ncols, int64_t chunk,
+                                                           float* out) {
+  __shared__ double red[8][32];
+  const int cl = threadIdx.x & 31, gq = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
+  const int64_t r0 = (int64_t)blockIdx.y * chunk, r1 = min(nb, r0 + chunk);
+  double s = 0.0;
+  if (c < ncols)
+    for (int64_t r = r0 + gq; r < r1; r += 8) s += part[r * ncols + c];
+  red[gq][cl] = s;
+  __syncthreads();
+  if (gq == 0 && c < ncols) {
+    double t = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += red[k][cl];
+    out[(int64_t)blockIdx.y * ncols + c] = (float)t;
+  }
+}
+
+extern "C" int64_t sm_linear_bn_stats_workspace_bytes(int M, int N) {
+  return ((int64_t)(M + 63) / 64) * 2 * N * 4 + (int64_t)LBS_CHUNKS * 2 * N * 4 + 2 * (int64_t)N * 8 + 64;
+}
+
+extern "C" int sm_bn_stats_from_partials(const float* part, int64_t nrows, int C, int64_t M, float* mean,
+                                         float* rstd, float* run_mean, float* run_var, int64_t* num_batches_tracked,
+                                         float momentum, float eps, int updates, void* ws, int64_t ws_bytes,
+                                         hipStream_t st);
+
+extern "C" int sm_linear_bn_stats(int M, int N, int K, const void* x, const void* w, void* y, float* mean, float* rstd,
+                                  float* run_mean, float* run_var, int64_t* num_batches_tracked, float momentum,
+                                  float eps, int updates, void* ws, int64_t ws_bytes, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return -2;
+  if (K <= 0 || K % 8 || N % 8 || (((uintptr_t)x | (uintptr_t)w | (uintptr_t)y) & 15)) return -2;
+  if (ws_bytes < sm_linear_bn_stats_workspace_bytes(M, N)) return -4;
+  const int64_t nparts = (M + 63) / 64;
+  float* part = (float*)ws;
+  float* part2 = part + nparts * 2 * N;
+  void* fin = (void*)(((uintptr_t)(part2 + (int64_t)LBS_CHUNKS * 2 * N) + 15) & ~(uintptr_t)15);
+  GemmArgs g{};
+  g.M = M; g.N = N; g.K = K; g.A = x; g.lda = K; g.B = w; g.ldb = K; g.C = y; g.ldc = N;
+  g.alpha = 1.f; g.beta = 0.f; g.rows_per_group = 1; g.k_begin = 0; g.k_chunk = K;
+  g.stat_part = part;
+  launch_bf16<true, true, __bf16, true>(g, 1, stream);
+  SM_CHECK_LAUNCH();
+  const int64_t chunk = (nparts + LBS_CHUNKS - 1) / LBS_CHUNKS;
+  const int nch = (int)((nparts + chunk - 1) / chunk);
+  hipLaunchKernelGGL(rowchunk_sum_kernel, dim3((2 * N + 31) / 32, nch), dim3(256), 0, stream, part, nparts, 2 * N,
+                     chunk, part2);
+  SM_CHECK_LAUNCH();
+  return sm_bn_stats_from_partials(part2, nch, N, M, mean, rstd, run_mean, run_var, num_batches_tracked, momentum,
+                                   eps, updates, fin, 2 * (int64_t)N * 8, stream);
 }
 
 extern "C" int64_t sm_linear_dw_se_workspace_bytes(int rows, int nout, int nin) {

@@ -57,6 +57,9 @@ _SIGS = {
     "sm_linear_dw_bias": (_c_i32, [_c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_i64, _c_p]),
     "sm_linear_dw_bias_gelu": (_c_i32, [_c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_f32, _c_u64, _c_p, _c_p, _c_i32, _c_p,
                                         _c_i64, _c_p]),
+    "sm_linear_bn_stats_workspace_bytes": (_c_i64, [_c_i32, _c_i32]),
+    "sm_linear_bn_stats": (_c_i32, [_c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_f32,
+                                    _c_f32, _c_i32, _c_p, _c_i64, _c_p]),
     "sm_linear_se": (_c_i32, [_c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_i32, _c_p,
                               _c_p]),
     "sm_linear_dw_se_workspace_bytes": (_c_i64, [_c_i32, _c_i32, _c_i32]),

@@ -179,13 +179,17 @@ class MBConvFn(torch.autograd.Function):
         Fr, H, Wd, Cin = x.shape
         mid, Cout, s = st.mid, st.cout, st.stride
         x2d = x.reshape(-1, Cin)
-        a1 = K.linear(x2d, W(w_exp, mode).view(mid, Cin))
         Ho, Wo = (H - 1) // s + 1, (Wd - 1) // s + 1
         fused = mode.bf16 and mid % 32 == 0
+        if fused and st.bn0.training:   # expand conv + BN0 statistics from its epilogue
+            a1, m0, r0 = K.linear_bn_stats(x2d, W(w_exp, mode).view(mid, Cin), st.bn0, st.bn_updates)
+        else:
+            a1 = K.linear(x2d, W(w_exp, mode).view(mid, Cin))
         if fused:
             # BN0 + GELU folded into the depthwise conv's loads, BN2 statistics produced
             # by it, BN2 + GELU folded into the SE reads: no act(a1) / act(a2) in HBM
-            m0, r0 = _bn_params(a1, st.bn0, st.bn_updates)
+            if not st.bn0.training:
+                m0, r0 = _bn_params(a1, st.bn0, st.bn_updates)
             act0 = (m0, r0, g0.detach(), b0.detach(), True)
             if st.bn2.training:
                 a2, m2, r2 = K.dwconv_fused(a1, act0, w_dw.detach().view(mid, 9), Fr, H, Wd, mid, s,
@@ -368,9 +372,10 @@ class BlockFn(torch.autograd.Function):
         del dhpre
         regs1 = st.drop1 > 0 or st.dp1 is not None
         C = x2.shape[1]
-        if act == torch.bfloat16 and C in (192, 384) and (regs1 or x2.dtype != act):
-            # the branch's bf16 copy of dx (cast + dropout / DropPath backward) from the
-            # LayerNorm backward's own pass
+        if act == torch.bfloat16 and C in (192, 384) and x2.dtype != act:
+            # fp32 stream (decoder): the branch's bf16 copy of dx (cast + dropout backward)
+            # from the LayerNorm backward's own pass.  (On the bf16 encoder stream, where only
+            # the DropPath scale remains, the separate pass measured cheaper.)
             dx2, dxb = K.layernorm_bwd_branch(dln2, x2, mu2, rs2, ln2w.detach(), G(ln2w), G(ln2b), dres=dout,
                                               drop_p=st.drop1, seed=st.seed1, row_scale=st.dp1, rows_per_group=L)
             del dln2

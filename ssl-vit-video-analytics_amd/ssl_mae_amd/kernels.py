@@ -106,6 +106,26 @@ def linear_dw_bias(dy, x, grad_w, grad_b, gelu=None):
     return grad_w
 
 
+def linear_bn_stats(x, w, running_mean=None, running_var=None, momentum=0.1, eps=1e-5, updates=1,
+                    num_batches=None):
+    """y = x @ w^T (bf16) and the train-mode BatchNorm statistics of y from the GEMM's
+    epilogue (sm_linear_bn_stats; = linear + bn_stats without the read pass of y).
+    Returns (y, mean, rstd)."""
+    _chk(x, w)
+    M, Kd = x.shape
+    N = w.shape[0]
+    if w.shape[1] != Kd or x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
+        raise _lib.KernelError("linear_bn_stats: bf16 x [M,K], w [N,K]")
+    y = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+    mean = torch.empty(N, dtype=torch.float32, device=x.device)
+    rstd = torch.empty(N, dtype=torch.float32, device=x.device)
+    nbytes = query("sm_linear_bn_stats_workspace_bytes", M, N)
+    ws = _ws(nbytes, x.device)
+    call("sm_linear_bn_stats", M, N, Kd, ptr(x), ptr(w), ptr(y), ptr(mean), ptr(rstd), ptr(running_mean),
+         ptr(running_var), ptr(num_batches), float(momentum), float(eps), int(updates), ptr(ws), nbytes, stream())
+    return y, mean, rstd
+
+
 def linear_se(a2, w, act, gate, hw):
     """y [M,N] bf16 = h3 @ w^T with h3 = se_scale(a2, gate, act) formed in the GEMM's
     A-operand loads (sm_linear_se; bit-identical to se_fwd's h3 + linear).  a2 [M,C] bf16,

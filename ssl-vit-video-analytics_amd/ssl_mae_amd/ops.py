@@ -745,6 +745,27 @@ def se_scale(x, s, F, HW, C, act=None):
     return torch.ops.ssl_mae.se_scale(x, s, F, HW, C, *_act(act))
 
 
+@_op("linear_bn_stats", "(Tensor x, Tensor w, Tensor(a!)? running_mean, Tensor(b!)? running_var, float momentum, "
+                        "float eps, int updates, Tensor(c!)? num_batches_tracked) -> (Tensor, Tensor, Tensor)",
+     ("running_mean", "running_var", "num_batches_tracked"))
+def _linear_bn_stats(x, w, running_mean, running_var, momentum, eps, updates, num_batches_tracked):
+    return _K.linear_bn_stats(x, w, running_mean, running_var, momentum, eps, updates, num_batches_tracked)
+
+
+@_linear_bn_stats.register_fake
+def _(x, w, *a):
+    N = w.shape[0]
+    return (x.new_empty((x.shape[0], N), dtype=torch.bfloat16), x.new_empty(N, dtype=torch.float32),
+            x.new_empty(N, dtype=torch.float32))
+
+
+def linear_bn_stats(x, w, bn, updates=1):
+    """Linear (1x1 conv) + the train-mode statistics of its BatchNorm from the GEMM's
+    epilogue; bn = the BatchNorm2d module (running statistics updated `updates` times)."""
+    return torch.ops.ssl_mae.linear_bn_stats(x, w, bn.running_mean, bn.running_var, float(bn.momentum),
+                                             float(bn.eps), int(updates), bn.num_batches_tracked)
+
+
 @_op("linear_se", "(Tensor a2, Tensor w, Tensor act_mean, Tensor act_rstd, Tensor act_w, Tensor act_b, "
                   "bool act_gelu, Tensor gate, int hw) -> Tensor")
 def _linear_se(a2, w, am, ar, aw, ab, ag, gate, hw):

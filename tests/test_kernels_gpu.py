@@ -771,6 +771,33 @@ def test_linear_dw_se_operand(Fr, HW, N, C, acc):
         assert rel_err(h3.float(), hh) < 1e-2
 
 
+@pytest.mark.parametrize("M,N,Kd,upd", [(100000, 384, 96, 2), (1000, 384, 96, 1), (100, 96, 64, 1), (4097, 40, 32, 2),
+                                        (12544 * 32, 384, 96, 2)])
+def test_linear_bn_stats(M, N, Kd, upd):
+    """Expand conv + its BatchNorm statistics from the GEMM epilogue (sm_linear_bn_stats):
+    y bit-identical to linear(), mean / rstd / running statistics within fp32 rounding of
+    bn_stats() over the same stored y (different fixed summation order), and
+    num_batches_tracked advanced `upd` times.  Shapes: ragged M (partial tiles and 64-row
+    slabs past M), the BM = 128 tile (M < 192), a ragged output width (N = 40)."""
+    kk = KK()
+    x = rnd(M, Kd, dtype=torch.bfloat16, seed=200).to(DEV)
+    w = rnd(N, Kd, dtype=torch.bfloat16, seed=201, scale=0.3).to(DEV)
+    rm1, rv1 = torch.full((N,), 0.1, device=DEV), torch.full((N,), 2.0, device=DEV)
+    rm2, rv2 = rm1.clone(), rv1.clone()
+    nb1 = torch.zeros((), dtype=torch.int64, device=DEV)
+    nb2 = nb1.clone()
+    y1 = kk.linear(x, w)
+    m1, r1 = kk.bn_stats(y1, rm1, rv1, 0.1, 1e-5, upd, nb1)
+    y2, m2, r2 = kk.linear_bn_stats(x, w, rm2, rv2, 0.1, 1e-5, upd, nb2)
+    assert torch.equal(y1, y2)
+    assert rel_err(m2, m1) < 1e-5 and rel_err(r2, r1) < 1e-5
+    assert rel_err(rm2, rm1) < 1e-5 and rel_err(rv2, rv1) < 1e-5
+    assert int(nb2) == upd == int(nb1)
+    yf = y1.float()
+    assert rel_err(m2, yf.mean(0)) < 1e-4
+    assert rel_err(r2, 1.0 / torch.sqrt(yf.var(0, unbiased=False) + 1e-5)) < 1e-4
+
+
 @pytest.mark.parametrize("Fr,HW,N,C", [(3, 128, 96, 384), (2, 256, 192, 768), (16, 12544, 96, 384),
                                        (5, 384, 40, 64), (1, 128, 8, 1536)])
 def test_linear_se_operand(Fr, HW, N, C):
