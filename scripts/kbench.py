@@ -147,8 +147,10 @@ def dwse(args):
             t3 = timeit(lambda: K.linear_se(a2, w, act, K.se_fwd(a2, Fn, HW, C, w1, w2, act=act, want_y=False)[3],
                                             HW), args.iters)
             t4 = timeit(lambda: K.se_fwd(a2, Fn, HW, C, w1, w2, act=act, want_y=False), args.iters)
+            gate = K.se_fwd(a2, Fn, HW, C, w1, w2, act=act, want_y=False)[3]
+            t5 = timeit(lambda: K.linear_se(a2, w, act, gate, HW), args.iters)
             print(f"{name} fwd: se_fwd + proj {t2:7.3f} ms | se gate + proj(se operand) {t3:7.3f} ms "
-                  f"(se gate alone {t4:7.3f} ms)", flush=True)
+                  f"(se gate alone {t4:7.3f} ms; proj(se operand) {t5:7.3f} ms)", flush=True)
         del a2, dy
         torch.cuda.empty_cache()
 
