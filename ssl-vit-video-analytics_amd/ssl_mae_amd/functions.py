@@ -198,7 +198,7 @@ class MBConvFn(torch.autograd.Function):
                 a2 = K.dwconv_fused(a1, act0, w_dw.detach().view(mid, 9), Fr, H, Wd, mid, s)
                 m2, r2 = K.bn_eval_params(st.bn2)
             act2 = (m2, r2, g2.detach(), b2.detach(), True)
-            if (Ho * Wo) % 128 == 0 and mid % 64 == 0 and mid <= 1536:
+            if (Ho * Wo) % 128 == 0 and mid % 64 == 0 and mid <= 1536 and Cout <= 128:
                 # SE gate only; the projection GEMM forms h3 = act(a2) * gate in its operand
                 # loads (no h3 round trip; bit-identical to se_fwd's h3 + linear)
                 pooled, h1se, gate = K.se_gate(a2, Fr, Ho * Wo, mid, w_fc0.detach(), w_fc2.detach(), act=act2)
