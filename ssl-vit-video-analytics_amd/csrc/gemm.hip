@@ -55,7 +55,7 @@ struct GemmArgs {
   ChanAffine xb_act;
   const float* xb_gate;
   int xb_hw;
-  // BatchNorm statistics of the bf16 output (sm_linear_bn_stats): per-wave column sums
+  // BatchNorm statistics of the bf16 output (IMP 8, sm_linear_bn_stats): per-wave column sums
   // and sums of squares of the stored values, [m-tile x waves along M][2][N]
   float* stat_part;
 };
@@ -233,7 +233,7 @@ SM_DEV void stage_put(const RowStage& rs, int region, int j, int p, int h, int l
 
 // Epilogue of one wave's (32 MI) x (32 NJ) tile from the (swapped-operand) accumulators.  stage:
 // non-null -> RowStage stores (VEC, non-split-K path); zs: the split-K slab of this block.
-template <typename TC, bool VEC, int MI = 2, int NJ = 2>
+template <typename TC, bool VEC, int MI = 2, int NJ = 2, bool STATS = false>
 SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[MI][NJ], int m0, int n0,
                                                          int wm, int wn, int l, int zs, char* stage = nullptr) {
   // The MFMAs run with swapped operands (D = B_frag x A_frag), so each lane owns
@@ -394,11 +394,11 @@ SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x
       const int64_t r0 = m0 + wm + 32 * i;
       const int c0 = n0 + wn;
       if (g.aux && (g.epi & 1)) rs_.flush<TC>(1, (TC*)g.aux, g.ldc, r0, c0, g.M, g.N, l);
-      if (g.stat_part) rs_.flush<TC, true>(0, (TC*)g.C, g.ldc, r0, c0, g.M, g.N, l, st1, st2);
+      if constexpr (STATS) rs_.flush<TC, true>(0, (TC*)g.C, g.ldc, r0, c0, g.M, g.N, l, st1, st2);
       else rs_.flush<TC>(0, (TC*)g.C, g.ldc, r0, c0, g.M, g.N, l);
     }
   }
-  if (stage && sizeof(TC) == 2 && g.stat_part && l < 8 && m0 + wm < g.M) {   // this wave's 64 rows x 64 cols
+  if (STATS && stage && sizeof(TC) == 2 && l < 8 && m0 + wm < g.M) {   // this wave's 64 rows x 64 cols
     const int wrow = (m0 + wm) >> 6;                         // part row = 64-row slab of the output
     const int col = n0 + wn + 8 * l;
     if (col < g.N) {
@@ -754,7 +754,8 @@ struct XformColsB {
   }
 };
 
-// IMP: 0 plain operands; 1 A is the implicit im2col of a conv (ConvRowsA);
+// IMP: 0 plain operands (8: plus the output's BatchNorm statistics in the epilogue,
+// sm_linear_bn_stats); 1 A is the implicit im2col of a conv (ConvRowsA);
 // 2 B is (ConvColsB); 5 / 7 B is formed on load (XformColsB); 6 A (K-major) is the
 // SE output formed on load (below).
 // (IMP 5: the activation's registers do not fit beside the staging set at 4 waves /
@@ -916,7 +917,7 @@ __global__ __launch_bounds__(BMV * 2, (BMV == 256 && IMP != 5 && IMP != 6 && IMP
     }
     __syncthreads();
   }
-  gemm_epilogue<TC, VEC>(g, acc, m0, n0, wm, wn, l, zs, lds + w * 8192);
+  gemm_epilogue<TC, VEC, 2, 2, IMP == 8>(g, acc, m0, n0, wm, wn, l, zs, lds + w * 8192);
 }
 
 // ============================================================ f32 MFMA kernel
@@ -1391,7 +1392,13 @@ extern "C" int sm_linear_bn_stats(int M, int N, int K, const void* x, const void
   g.M = M; g.N = N; g.K = K; g.A = x; g.lda = K; g.B = w; g.ldb = K; g.C = y; g.ldc = N;
   g.alpha = 1.f; g.beta = 0.f; g.rows_per_group = 1; g.k_begin = 0; g.k_chunk = K;
   g.stat_part = part;
-  launch_bf16<true, true, __bf16, true>(g, 1, stream);
+  const int tiles_n = (N + 127) / 128;
+  if (gemm_variant(M, N, K) == 2)
+    hipLaunchKernelGGL((gemm_bf16_v2<true, true, __bf16, true, 256, 8>), dim3(tiles_n * ((M + 255) / 256)), dim3(512),
+                       0, stream, g);
+  else
+    hipLaunchKernelGGL((gemm_bf16_v2<true, true, __bf16, true, 128, 8>), dim3(tiles_n * ((M + 127) / 128)), dim3(256),
+                       0, stream, g);
   SM_CHECK_LAUNCH();
   const int64_t chunk = (nparts + LBS_CHUNKS - 1) / LBS_CHUNKS;
   const int nch = (int)((nparts + chunk - 1) / chunk);
