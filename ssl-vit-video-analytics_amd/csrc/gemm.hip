@@ -233,7 +233,7 @@ SM_DEV void stage_put(const RowStage& rs, int region, int j, int p, int h, int l
 
 // Epilogue of one wave's (32 MI) x (32 NJ) tile from the (swapped-operand) accumulators.  stage:
 // non-null -> RowStage stores (VEC, non-split-K path); zs: the split-K slab of this block.
-template <typename TC, bool VEC, int MI = 2, int NJ = 2, bool STATS = false>
+template <typename TC, bool VEC, int MI = 2, int NJ = 2, bool STATS = false, bool AUXS = false>
 SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[MI][NJ], int m0, int n0,
                                                          int wm, int wn, int l, int zs, char* stage = nullptr) {
   // The MFMAs run with swapped operands (D = B_frag x A_frag), so each lane owns
@@ -311,6 +311,29 @@ SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x
     if (!rok && !stage) continue;
     const float rs = (g.row_scale && rok) ? g.row_scale[row / g.rows_per_group] : 1.f;
     const uint32_t rb = drop_rowbase(s32, (uint64_t)row);
+    if constexpr (AUXS && sizeof(TC) == 2) {
+      // GELU backward's pre-activation (aux) for this 32-row x 64-column image, loaded as
+      // 8 rows x 128 B per instruction into stage region 1 (whole lines, where a run per
+      // lane touches 32 rows x 32 B), then read back per run in the stage_put layout
+      if (stage) {
+        const int c = l & 7;
+        uint4 av[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = (l >> 3) + 8 * q;
+          const int64_t rowq = m0 + wm + 32 * i + r;
+          const int colq = n0 + wn + 8 * c;
+          av[q] = (rowq < g.M && colq < g.N) ? *(const uint4*)((const TC*)g.aux + rowq * g.ldc + colq)
+                                              : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = (l >> 3) + 8 * q;
+          *(uint4*)(stage + 4096 + r * 128 + ((c ^ ((r >> 1) & 7)) << 4)) = av[q];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+    }
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       uint4 rr[2][RW];   // the residual runs of this (row, j), in flight before the stores (R may alias C)
@@ -350,7 +373,12 @@ SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x
         const int64_t idx = row * g.ldc + col;
         if (g.epi & 4) {   // GELU backward: the saved pre-activation run of this (row, cols)
           float pre[8];
-          load8((const TC*)g.aux + idx, pre);
+          if (AUXS && sizeof(TC) == 2 && stage) {
+            const int rr_ = l & 31, ch_ = 4 * j + 2 * p + h;
+            load8((const __bf16*)(stage + 4096 + rr_ * 128 + ((ch_ ^ ((rr_ >> 1) & 7)) << 4)), pre);
+          } else {
+            load8((const TC*)g.aux + idx, pre);
+          }
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] *= gelu_grad(pre[e]);
         }
@@ -755,7 +783,8 @@ struct XformColsB {
 };
 
 // IMP: 0 plain operands (8: plus the output's BatchNorm statistics in the epilogue,
-// sm_linear_bn_stats); 1 A is the implicit im2col of a conv (ConvRowsA);
+// sm_linear_bn_stats; 9: the GELU-backward pre-activation staged through LDS by whole
+// lines); 1 A is the implicit im2col of a conv (ConvRowsA);
 // 2 B is (ConvColsB); 5 / 7 B is formed on load (XformColsB); 6 A (K-major) is the
 // SE output formed on load (below).
 // (IMP 5: the activation's registers do not fit beside the staging set at 4 waves /
@@ -917,7 +946,7 @@ __global__ __launch_bounds__(BMV * 2, (BMV == 256 && IMP != 5 && IMP != 6 && IMP
     }
     __syncthreads();
   }
-  gemm_epilogue<TC, VEC, 2, 2, IMP == 8>(g, acc, m0, n0, wm, wn, l, zs, lds + w * 8192);
+  gemm_epilogue<TC, VEC, 2, 2, IMP == 8, IMP == 9>(g, acc, m0, n0, wm, wn, l, zs, lds + w * 8192);
 }
 
 // ============================================================ f32 MFMA kernel
@@ -1231,7 +1260,15 @@ static int gemm_run(int ab_dtype, int c_dtype, int a_layout, int b_layout, int M
     g.k_begin = 0; g.k_chunk = K;
   }
   int rc;
-  if (a_layout == 0 && b_layout == 0) rc = launch_layout<true, true>(ab_dtype, c_dtype, g, splits, stream);
+  if ((epi & 4) && ab_dtype == SM_BF16 && c_dtype == SM_BF16 && a_layout == 0 && b_layout == 1 && splits == 1 &&
+      !((N & 7) || (ldc & 7)) && K > 0) {   // the GELU-backward dX GEMM: IMP 9 epilogue
+    const int v = gemm_variant(M, N, K);
+    const int tiles = ((N + 127) / 128) * ((M + variant_bm(v) - 1) / variant_bm(v));
+    if (v == 2) hipLaunchKernelGGL((gemm_bf16_v2<true, false, __bf16, true, 256, 9>), dim3(tiles), dim3(512), 0, stream, g);
+    else hipLaunchKernelGGL((gemm_bf16_v2<true, false, __bf16, true, 128, 9>), dim3(tiles), dim3(256), 0, stream, g);
+    SM_CHECK_LAUNCH();
+    rc = 0;
+  } else if (a_layout == 0 && b_layout == 0) rc = launch_layout<true, true>(ab_dtype, c_dtype, g, splits, stream);
   else if (a_layout == 0 && b_layout == 1) rc = launch_layout<true, false>(ab_dtype, c_dtype, g, splits, stream);
   else if (a_layout == 1 && b_layout == 0) rc = launch_layout<false, true>(ab_dtype, c_dtype, g, splits, stream);
   else rc = launch_layout<false, false>(ab_dtype, c_dtype, g, splits, stream);
