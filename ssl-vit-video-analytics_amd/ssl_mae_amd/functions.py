@@ -104,9 +104,14 @@ class StemFn(torch.autograd.Function):
         act = mode.act
         col1, (Fr, Ho, Wo) = K.stem_im2col(clip, act)
         w1p = K.conv_wpack(w1.detach(), 32, 0, act)
-        a1 = K.linear(col1, w1p)
-        del col1
-        h1, m1, r1 = _bn_forward(a1, st.bn1, gelu=True)
+        if mode.bf16 and st.bn1.training:   # conv1 + BN1 statistics from the GEMM epilogue
+            a1, m1, r1 = K.linear_bn_stats(col1, w1p, st.bn1)
+            del col1
+            h1 = K.bn_apply(a1, m1, r1, g1.detach(), b1.detach(), gelu=True)
+        else:
+            a1 = K.linear(col1, w1p)
+            del col1
+            h1, m1, r1 = _bn_forward(a1, st.bn1, gelu=True)
         w2p = K.conv_wpack(w2.detach(), 432, 1, act)
         if mode.bf16:       # conv2 as a GEMM over the implicit im2col of h1 (no 9x buffer)
             a2 = K.conv3x3_fwd(h1, w2p, Fr, Ho, Wo, 48, 96)
