@@ -422,6 +422,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(AttnArgs a) {
       for (int j = 0; j < 8; ++j) { kf[s][j] = (__bf16)0.f; vf[s][j] = (__bf16)0.f; }
     }
   }
+  // K pre-scaled by scale * log2(e) (once, in registers) and the S accumulator started
+  // at -LSE2 of its query row: the MFMA leaves the exp2 argument itself, one VALU op per
+  // score fewer than exp2(fma(S, c, -LSE2)) (the kernels are bound by VALU issue).
+  // dK uses Q from LDS, unscaled.
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) kf[s][j] = (__bf16)((float)kf[s][j] * (a.scale * LOG2E));
   Stager<D, QT> sq, sd;
   sq.init(ldq);
   sd.init(C);
@@ -436,7 +444,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(AttnArgs a) {
   for (int t = 0; t < D / 32; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) { dk[t][r] = 0.f; dv[t][r] = 0.f; }
-  const float c = a.scale * LOG2E;
   const float lkeep = DROP ? log2f(1.f - a.drop_p) : 0.f;   // log2 of 1/ks
   const float dkeep = DROP ? 1.f - a.drop_p : -1.f;         // stored Delta factor
   const uint32_t dthr = attn_thr(a.drop_p);
@@ -449,7 +456,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(AttnArgs a) {
   // S = Q K^T and dP = dO V^T for query rows q0 + 32u .. +31 (keys on lanes)
   auto sdp = [&](int u, f32x16& sa, f32x16& da) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) sa[r] = 0.f;
+    for (int g = 0; g < 4; ++g) {   // -LSE2 of rows 32u + 8g + 4h + j
+      const float4 a4 = *(const float4*)&llse[32 * u + 8 * g + 4 * h];
+      sa[4 * g] = -a4.x; sa[4 * g + 1] = -a4.y; sa[4 * g + 2] = -a4.z; sa[4 * g + 3] = -a4.w;
+    }
     if (DROP) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) da[r] = 0.f;
@@ -474,8 +484,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(AttnArgs a) {
       uint32_t kb4 = 0;
       if (DROP)
         kb4 = keep_bytes(keep_flags(quad_transpose_bytes(mix24(dlb + (uint32_t)(q0 + 32 * u + 8 * g) * AG), sel1, sel2), dthr));
-      const float4 a4 = *(const float4*)&llse[32 * u + 8 * g + 4 * h];
-      const float lse4[4] = {a4.x, a4.y, a4.z, a4.w};
       float del4[4] = {0.f, 0.f, 0.f, 0.f};
       if (DROP) {
         const float4 b4 = *(const float4*)&ldel[32 * u + 8 * g + 4 * h];
@@ -484,7 +492,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(AttnArgs a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int r = 4 * g + j;
-        const float p = __builtin_amdgcn_exp2f(fmaf(sa[r], c, -lse4[j]));
+        const float p = __builtin_amdgcn_exp2f(sa[r]);
         if (DROP) {
           const float pk = keep_sel(p, kb4, j);
           pv[r] = pk;
@@ -592,6 +600,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16(AttnArgs a) {
   }
   const float dl = halves_sum(dpart);
   if (qok && h == 0) a.delta[((int64_t)n * a.H + hd) * a.L + q] = dl;
+  // Q pre-scaled by scale * log2(e) in registers and S started at -LSE2: the MFMA leaves
+  // the exp2 argument (as in the dK/dV kernel); dQ = dS K needs no Q
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qf[s][j] = (__bf16)((float)qf[s][j] * (a.scale * LOG2E));
   Stager<D, KT> stg;
   stg.init(ldq);
   int roff[D / 16], tlo[D / 32], thi[D / 32];
@@ -604,7 +618,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16(AttnArgs a) {
   for (int t = 0; t < D / 32; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) dq[t][r] = 0.f;
-  const float c = a.scale * LOG2E;
   const float ks = DROP ? 1.f / (1.f - a.drop_p) : 1.f;
   const uint32_t dlb = seed32(a.seed) + (uint32_t)((uint64_t)(n * a.H + hd) * a.L + q) * AG + (uint32_t)h * AC;
   const uint32_t dthr = attn_thr(a.drop_p);
@@ -626,7 +639,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16(AttnArgs a) {
     for (int u = 0; u < 2; ++u) {
       f32x16 sacc, dpacc;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) { sacc[r] = 0.f; dpacc[r] = 0.f; }
+      for (int r = 0; r < 16; ++r) { sacc[r] = -lse2; dpacc[r] = 0.f; }
 #pragma unroll
       for (int s = 0; s < D / 16; ++s) {
         sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_b128(lk, roff[s] + u * RB), qf[s], sacc, 0, 0, 0);
@@ -644,7 +657,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16(AttnArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int r = 4 * g + j;
-          const float p = __builtin_amdgcn_exp2f(fmaf(sacc[r], c, -lse2));
+          const float p = __builtin_amdgcn_exp2f(sacc[r]);
           const float dp = dpacc[r];
           if (DROP) dpacc[r] = p * fmaf(keep_sel(dp, hv, j), ks, -dl);
           else dpacc[r] = p * (dp - dl);
