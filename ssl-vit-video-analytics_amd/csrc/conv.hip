@@ -371,7 +371,9 @@ struct DwfBlock {
   }
 };
 
-template <int S>
+// STATS: accumulate the BatchNorm partials of y (false for the lite-resident recompute and
+// the data-gradient use, which pass part = null: two VALU ops per output fewer)
+template <int S, bool STATS = true>
 __global__ __launch_bounds__(256, 2) void dwf_fwd_kernel(const __bf16* x, ChanAffine act, const float* w,
                                                          __bf16* y, float* part, int H, int W, int C, int Ho,
                                                          int Wo, int remap) {
@@ -453,14 +455,16 @@ __global__ __launch_bounds__(256, 2) void dwf_fwd_kernel(const __bf16* x, ChanAf
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           r8[j] = (float)(__bf16)acc[p][j];
-          s8[j] += r8[j];
-          q8[j] += r8[j] * r8[j];
+          if (STATS) {
+            s8[j] += r8[j];
+            q8[j] += r8[j] * r8[j];
+          }
         }
         store8(y + ((f * Ho + yo) * Wo + xo0 + p) * C + cbase, r8);
       }
     }
   }
-  if (!part) return;
+  if (!STATS || !part) return;
   __syncthreads();                              // ring dead: reuse for the reduction
   float* red = (float*)lds;                     // [256][16]
 #pragma unroll
@@ -1409,12 +1413,18 @@ extern "C" int sm_dwconv_fused_fwd(int F, int H, int W, int C, int stride, const
   const dim3 grid((C / DWF_CB) * F);
   const size_t lds = dwf_lds_bytes(W, stride);
   const int remap = dwf_remap();
-  if (stride == 1)
+  if (stride == 1 && part)
     hipLaunchKernelGGL((dwf_fwd_kernel<1>), grid, dim3(256), lds, st, (const __bf16*)x, act, w, (__bf16*)y, part,
                        H, W, C, Ho, Wo, remap);
-  else
+  else if (stride == 1)
+    hipLaunchKernelGGL((dwf_fwd_kernel<1, false>), grid, dim3(256), lds, st, (const __bf16*)x, act, w, (__bf16*)y,
+                       part, H, W, C, Ho, Wo, remap);
+  else if (part)
     hipLaunchKernelGGL((dwf_fwd_kernel<2>), grid, dim3(256), lds, st, (const __bf16*)x, act, w, (__bf16*)y, part,
                        H, W, C, Ho, Wo, remap);
+  else
+    hipLaunchKernelGGL((dwf_fwd_kernel<2, false>), grid, dim3(256), lds, st, (const __bf16*)x, act, w, (__bf16*)y,
+                       part, H, W, C, Ho, Wo, remap);
   SM_CHECK_LAUNCH();
   return 0;
 }
@@ -1445,7 +1455,7 @@ extern "C" int sm_dwconv_fused_bwd(int F, int H, int W, int C, int stride, const
     if (stride == 1) {
       hipLaunchKernelGGL(dw_rotate_kernel, dim3((C * 9 + 255) / 256), dim3(256), 0, st, w, wrot, C * 9);
       ChanAffine none{nullptr, nullptr, nullptr, nullptr, 0};
-      hipLaunchKernelGGL((dwf_fwd_kernel<1>), dim3((C / DWF_CB) * F), dim3(256), lds, st, (const __bf16*)dy, none,
+      hipLaunchKernelGGL((dwf_fwd_kernel<1, false>), dim3((C / DWF_CB) * F), dim3(256), lds, st, (const __bf16*)dy, none,
                          (const float*)wrot, (__bf16*)dx, (float*)nullptr, Ho, Wo, C, H, W, dwf_remap());
     } else {
       const int64_t total = (int64_t)F * H * ((W + DW_PX - 1) / DW_PX) * (C / 8);
