@@ -1,5 +1,6 @@
 # Same-box A/B of the full bench step: ab_base/ (a git worktree of an older commit with its
 # own built library) against this tree, alternating, cpu baseline off.
+# baseline tree: git worktree add -f ab_base <commit> && (cd ab_base && python -c "import __graft_entry__ as g; g.build()")
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 TAG=${1:-ab}

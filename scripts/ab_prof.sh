@@ -1,5 +1,6 @@
 # Same-box per-kernel A/B: rocprofv3 kernel stats of the bench step for ab_base/ and this tree
 set -e
+# baseline tree: git worktree add -f ab_base <commit> && (cd ab_base && python -c "import __graft_entry__ as g; g.build()")
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 TAG=${1:-abp}
