@@ -116,23 +116,6 @@ __global__ void pos_blend_spos_kernel(const TG* dx, const uint8_t* mask, int F, 
   }
 }
 
-// dtpos[t][d] += sum_b pt[b*T+t][d];  dtok[d] += sum_f pm[f][d]
-__global__ void pos_blend_final_kernel(const float* pt, const float* pm, int B, int T, int D, float* dtpos,
-                                       float* dtok) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < T * D) {
-    const int t = i / D, d = i % D;
-    double s = 0.0;
-    for (int b = 0; b < B; ++b) s += pt[((int64_t)b * T + t) * D + d];
-    dtpos[i] += (float)s;
-  }
-  if (i < D) {
-    double s = 0.0;
-    for (int f = 0; f < B * T; ++f) s += pm[(int64_t)f * D + i];
-    dtok[i] += (float)s;
-  }
-}
-
 // ------------------------------------------------------------------ fused loss
 struct LossArgs {
   const void* pred;          // [B][T*L][192]
@@ -402,8 +385,10 @@ extern "C" int sm_pos_blend_bwd(int g_dtype, int y_dtype, const void* dx, const 
                                         L, D, pt, pm));
   DISPATCH1(g_dtype, hipLaunchKernelGGL(pos_blend_spos_kernel<T>, dim3(ew_blocks((int64_t)L * D)), dim3(256), 0,
                                         st, (const T*)dx, mask, F, L, D, dspos));
-  hipLaunchKernelGGL(pos_blend_final_kernel, dim3((T * D + 255) / 256 + 1), dim3(256), 0, st, pt, pm, B, T, D,
-                     dtpos, dtok);
+  // dtpos[t][d] += sum_b pt[b][t][d] and dtok[d] += sum_f pm[f][d]: fixed-order fp64 column
+  // reductions ([B][T*D] and [F][D] views), many threads per column instead of one
+  colred(pt, B, T * D, nullptr, dtpos, 1, st);
+  colred(pm, F, D, nullptr, dtok, 1, st);
   SM_CHECK_LAUNCH();
   return 0;
 }
