@@ -216,12 +216,17 @@ def main():
     Ld = T * (S // 8) ** 2
     if args.probe == "dec_attn_fwd":
         probe.wrap(K, "attn_fwd", lambda qkv, N, L, H, D, *a, **k: D == 64 and L == Ld)
-        flop_per_launch = 4.0 * B * 6 * Ld * Ld * 64
+        flop_per_launch = 4.0 * B * 6 * Ld * Ld * 64        # S = QK^T and O = PV
+        exec_flop_per_launch = flop_per_launch
     elif args.probe == "dec_attn_bwd":
         probe.wrap(K, "attn_bwd", lambda qkv, o, do, lse, N, L, H, D, *a, **k: D == 64 and L == Ld)
-        flop_per_launch = 14.0 * B * 6 * Ld * Ld * 64   # dK/dV pass (4 products) + dQ pass (3)
+        # training work = 3x forward, so the backward's algorithmic work
+        # is 2x the forward's 4*B*H*L^2*D (dV, dP, dQ, dK; the recompute of S is not
+        # counted).  The split dK/dV + dQ kernels execute 14*B*H*L^2*D (S and dP in both).
+        flop_per_launch = 8.0 * B * 6 * Ld * Ld * 64
+        exec_flop_per_launch = 14.0 * B * 6 * Ld * Ld * 64
     else:
-        flop_per_launch = None
+        flop_per_launch = exec_flop_per_launch = None
 
     ssl_cfg = cfg["ssl"]
     # rank-0 weights/buffers broadcast; bucketed RCCL all-reduce launched from the
@@ -270,7 +275,9 @@ def main():
                     "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None,
                     "avg_launch_ms": round(avg, 3), "launches": len(probe.pairs),
-                    "algorithmic_flop_per_launch": flop_per_launch}
+                    "algorithmic_flop_per_launch": flop_per_launch,
+                    "executed_flop_per_launch": exec_flop_per_launch,
+                    "executed_frac": round(exec_flop_per_launch / (avg * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4)}
             tr = pmc_traffic(args.probe, B, T, S)
             if tr:
                 roof.update(tr)
