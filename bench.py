@@ -87,11 +87,20 @@ def cpu_baseline(T, S, ratio):
 
 PROBE_KERNELS = {"dec_attn_fwd": "attn_fwd_bf16<64, true>",
                  "dec_attn_bwd": "attn_bwd_dq_bf16<64, true>+attn_bwd_dkdv_bf16<64, true>"}
-REFERENCE_CPU = {"value": 0.036, "unit": "clips/s", "cores": 8, "kind": "reference",
-                 "sample": "the reference's train_one_epoch path itself (fp32, dropout/DropPath on) at BASELINE "
-                           "config 1 (B=4, T=8, 224x224, mask 0.75): 102.5 / 110.7 s per step on the 8 Xeon "
-                           "cores of the build container (SURVEY.md §8(d)); the reference cannot travel to the "
-                           "GPU box"}
+def reference_cpu():
+    """The reference's own train_one_epoch timed on the build container's CPU cores at
+    BASELINE config 1 by scripts/ref_cpu_baseline.py (the reference cannot travel to
+    the GPU box); the newest committed profiles/*_ref_cpu_baseline.json."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_ref_cpu_baseline.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        out = {k: d[k] for k in ("value", "unit", "cores", "kind", "sample") if k in d}
+        out["source"] = os.path.relpath(f, ROOT)
+        return out
+    return None
 
 
 def pmc_traffic(probe, B, T, S):
@@ -320,7 +329,7 @@ def main():
             "peak_mem_gib": round(peak_mem, 1),
             "loss_first_last": [round(loss_vals[0], 5), round(loss_vals[-1], 5)],
             "cpu_baseline": cpu,
-            "cpu_baseline_reference": REFERENCE_CPU if not small else None,
+            "cpu_baseline_reference": reference_cpu() if not small else None,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -10,8 +10,10 @@ training-state file next to it with everything needed to continue bit-for-bit:
   optimizer    FusedAdamW state (per-name exp_avg / exp_avg_sq, step, hyper-params)
   scaler       GradScaler shim state
   epoch        last finished epoch
-  rng          torch CPU generator (drives the tube mask), device generator seeds,
-               numpy / python RNG (drive the loader's frame-index choice)
+  rng          torch CPU generator (drives the tube mask), device generators (seed
+               AND state/offset, so torch device RNG use after a resume continues the
+               stream), numpy / python RNG incl. python's cached gauss_next (drive the
+               loader's frame-index choice)
 
 Everything is a tensor / number / string, so `torch.load(..., weights_only=True)`
 reads it back.
@@ -29,10 +31,12 @@ def _rng_state():
     st = {"torch_cpu": torch.get_rng_state(),
           "numpy_keys": torch.from_numpy(np_state[1].astype(np.int64)),
           "numpy_pos": int(np_state[2]), "numpy_has_gauss": int(np_state[3]), "numpy_gauss": float(np_state[4]),
-          "python_version": int(py[0]), "python_state": torch.tensor(py[1], dtype=torch.int64)}
+          "python_version": int(py[0]), "python_state": torch.tensor(py[1], dtype=torch.int64),
+          "python_has_gauss": int(py[2] is not None), "python_gauss": float(py[2]) if py[2] is not None else 0.0}
     if torch.cuda.is_available():
         st["cuda_seeds"] = torch.tensor([g.initial_seed() for g in torch.cuda.default_generators],
                                         dtype=torch.int64)
+        st["cuda_states"] = [s.clone() for s in torch.cuda.get_rng_state_all()]
     return st
 
 
@@ -40,10 +44,13 @@ def _set_rng_state(st):
     torch.set_rng_state(st["torch_cpu"])
     np.random.set_state(("MT19937", st["numpy_keys"].numpy().astype(np.uint32), int(st["numpy_pos"]),
                          int(st["numpy_has_gauss"]), float(st["numpy_gauss"])))
-    random.setstate((int(st["python_version"]), tuple(int(v) for v in st["python_state"].tolist()), None))
+    gauss = float(st["python_gauss"]) if int(st.get("python_has_gauss", 0)) else None
+    random.setstate((int(st["python_version"]), tuple(int(v) for v in st["python_state"].tolist()), gauss))
     if "cuda_seeds" in st and torch.cuda.is_available():
         for g, s in zip(torch.cuda.default_generators, st["cuda_seeds"].tolist()):
             g.manual_seed(int(s))
+        if "cuda_states" in st and len(st["cuda_states"]) == torch.cuda.device_count():
+            torch.cuda.set_rng_state_all(st["cuda_states"])   # seed and offset
 
 
 def save_training_state(path, model, optimizer, scaler, epoch):

@@ -30,7 +30,7 @@ import torch
 import torch.nn as nn
 
 from . import ops as K    # every kernel launch through the torch.ops.ssl_mae dispatcher
-from .functions import Mode
+from .functions import Mode, splitmix64
 from .mae_vit_adapter import ensure_flat, next_seed_base
 from .tiny_vit import TinyViT
 
@@ -95,6 +95,15 @@ def tiny_vit_backbone(img_size=112, use_checkpoint=True, **kwargs):
                            num_heads=[3, 6, 12, 18], use_checkpoint=use_checkpoint, **kwargs)
 
 
+def frame_modes(mode, T):
+    """One Mode per per-frame backbone call of a train-mode forward: the same
+    precision, seed bases mixed with the time index so the DropPath masks of the T
+    calls are independent (the reference draws fresh masks on every backbone call).
+    Each call's checkpoint recompute / backward reuses its own Mode, so replay stays
+    exact."""
+    return [Mode(mode.bf16, splitmix64(mode.seed_base ^ splitmix64(0x5EED0000 + t))) for t in range(T)]
+
+
 class VideoClassifier(nn.Module):
     """train_finetune.py:19-40 with the MAE-pretrained TinyViT as backbone."""
 
@@ -113,8 +122,10 @@ class VideoClassifier(nn.Module):
         ensure_flat(bb, mode)
         if bb.training:
             # per-frame backbone calls as the reference (BatchNorm batch statistics and
-            # running-stat updates per time step)
-            feats = torch.stack([bb.embed(clip[:, :, t], mode)[0] for t in range(T)], dim=1)   # [B, T, D]
+            # running-stat updates per time step); each call draws its own DropPath masks
+            # (the reference's per-call torch RNG draws), so each gets its own seed base
+            feats = torch.stack([bb.embed(clip[:, :, t], m)[0] for t, m in enumerate(frame_modes(mode, T))],
+                                dim=1)   # [B, T, D]
         else:
             feats = bb.embed(clip, mode)[0].view(B, T, -1)       # frames b*T + t, one batch
         video_emb = SegMeanFn.apply(feats.reshape(B * T, -1), B, T)

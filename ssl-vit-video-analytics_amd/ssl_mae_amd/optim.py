@@ -94,8 +94,17 @@ class FlatParams:
             return
         for p in params:
             b = self.bucket_of.get(id(p))
-            if b is None or id(p) in self._finished:
+            if b is None:
                 continue
+            if id(p) in self._finished:
+                # a second gradient contribution after the bucket may already be in
+                # flight on the side stream: the reduced value would race the add
+                raise RuntimeError(
+                    f"FlatParams.done: parameter {self.names[self.index[id(p)]]} received gradient from more "
+                    "than one backward group in one step while bucketed all-reduce hooks are attached; the "
+                    "overlapped all-reduce supports exactly one gradient write per parameter per backward "
+                    "(run modules used several times per step without OverlappedGradAllReduce, e.g. with "
+                    "dist.GradAllReduce after the backward)")
             self._finished.add(id(p))
             self._pending[b] -= 1
             if self._pending[b] == 0:

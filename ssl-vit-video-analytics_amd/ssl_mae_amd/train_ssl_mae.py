@@ -12,15 +12,27 @@ TypeError prevents.  The loader is the MI355X clip pipeline of mae_loader
 ready fp32 clips (the reference's transform path) is accepted as well.  Every 10
 epochs the reference's encoder-only file is written, plus a full training-state
 file (`checkpoint.py`) that `--resume` continues from.
+
+Data parallel (north star; the reference is single-device, :132): launched under
+torchrun, `main()` runs one process per GPU (RCCL over xGMI, `dist.init_from_env`),
+shards the dataset with a DistributedSampler (`set_epoch` per epoch), starts every
+replica from rank 0's weights and all-reduces the gradients in buckets on a side
+stream during the backward (`dist.setup_data_parallel`).  BatchNorm keeps
+per-replica batch statistics.  The logged loss is the mean over ranks, the logged
+throughput the global samples/s; logs and checkpoints are written by rank 0 only.
+With one process it is exactly the single-device loop.
 """
 import argparse
 import logging
+import os
 import time
 from datetime import timedelta
 from pathlib import Path
 
 import torch
+import torch.distributed as dist
 
+from . import dist as smdist
 from . import ops as K    # every kernel launch through the torch.ops.ssl_mae dispatcher
 from .functions import mae_loss, masked_pred_std
 from .checkpoint import load_training_state, save_training_state
@@ -83,6 +95,20 @@ def _to_clip(batch, device, normalizer):
     return batch.to(device, non_blocking=True)
 
 
+def _world():
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+
+def _mean_over_ranks(t):
+    """Mean of a scalar tensor over the data-parallel ranks (the logged loss)."""
+    world = _world()
+    if world == 1:
+        return t
+    t = t.detach().clone()
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t / world
+
+
 def train_one_epoch(model, loader, optimizer, scaler, epoch, device, config, writer, logger, normalizer=None):
     model.train()
     if normalizer is None:
@@ -90,13 +116,14 @@ def train_one_epoch(model, loader, optimizer, scaler, epoch, device, config, wri
     ssl_cfg = config["ssl"]
     train_cfg = config["training"]
     num_steps = len(loader)
-    batch_size = train_cfg["batch_size"]
+    batch_size = train_cfg["batch_size"] * _world()      # global samples per step
     epoch_start = time.time()
     last_log = time.time()
     total_loss = 0.0
     for step, batch in enumerate(loader):
         clip = _to_clip(batch, device, normalizer)
         loss, pred, idx = train_step(model, clip, optimizer, scaler, ssl_cfg)
+        loss = _mean_over_ranks(loss)
         total_loss += loss.item()
         if step % train_cfg["log_interval"] == 0 and step > 0:
             now = time.time()
@@ -120,12 +147,21 @@ def build_model(cfg, device="cuda"):
     return TinyVideoMAE(encoder, cfg).to(device)
 
 
-def make_loader(ds, batch_size, num_workers=16, shuffle=True):
+def make_loader(ds, batch_size, num_workers=16, shuffle=True, sampler=None):
     """train_ssl_mae.py:154-161 (16 workers, pinned memory, prefetch 2) over the
-    uint8-frame dataset (collate_frames)."""
+    uint8-frame dataset (collate_frames); `sampler` (data parallel: a
+    DistributedSampler) replaces the shuffle."""
     kw = {"prefetch_factor": 2} if num_workers > 0 else {}
-    return torch.utils.data.DataLoader(ds, batch_size=batch_size, shuffle=shuffle, num_workers=num_workers,
-                                       pin_memory=True, collate_fn=collate_frames, **kw)
+    return torch.utils.data.DataLoader(ds, batch_size=batch_size, shuffle=shuffle and sampler is None,
+                                       sampler=sampler, num_workers=num_workers, pin_memory=True,
+                                       collate_fn=collate_frames, **kw)
+
+
+class _RankZeroLogger:
+    """Logger stand-in for ranks > 0 (the reference logs from its one process)."""
+
+    def info(self, *a, **k):
+        pass
 
 
 def main(argv=None):
@@ -135,18 +171,31 @@ def main(argv=None):
     ap.add_argument("--max-steps", type=int, default=None, help="stop each epoch after this many steps")
     args = ap.parse_args(argv)
     cfg = load_config(args.config)
+    rank, world = smdist.init_from_env()          # torchrun: one process per GPU (RCCL)
     set_seed(42)
-    device = torch.device("cuda")
-    logger, log_dir = setup_logger(cfg["training"]["save_dir"])
-    try:
-        from torch.utils.tensorboard import SummaryWriter
-        writer = SummaryWriter(log_dir=str(log_dir / "tensorboard"))
-    except Exception:
-        writer = NullWriter()
+    local = int(os.environ.get("LOCAL_RANK", "0")) if world > 1 else torch.cuda.current_device()
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if rank == 0:
+        logger, log_dir = setup_logger(cfg["training"]["save_dir"])
+        try:
+            from torch.utils.tensorboard import SummaryWriter
+            writer = SummaryWriter(log_dir=str(log_dir / "tensorboard"))
+        except Exception:
+            writer = NullWriter()
+    else:
+        logger, writer = _RankZeroLogger(), NullWriter()
     model = build_model(cfg, device)
+    if rank > 0:
+        # independent mask / frame-index streams per replica (rank 0 keeps the
+        # reference's set_seed(42) streams; weights come from rank 0's broadcast)
+        set_seed(42 + 1000 * rank)
     ds = LazyVideoMAEDataset(split_file=cfg["dataset"]["train_split"], clip_len=cfg["dataset"]["clip_len"],
                              stride=cfg["dataset"]["stride"], image_size=cfg["dataset"]["image_size"])
-    loader = make_loader(ds, cfg["training"]["batch_size"], int(cfg["training"].get("num_workers", 16)))
+    sampler = torch.utils.data.DistributedSampler(ds, num_replicas=world, rank=rank, shuffle=True, seed=42) \
+        if world > 1 else None
+    loader = make_loader(ds, cfg["training"]["batch_size"], int(cfg["training"].get("num_workers", 16)),
+                         sampler=sampler)
     if args.max_steps is not None:
         loader = _Limited(loader, args.max_steps)
     optimizer = FusedAdamW(model.parameters(), lr=float(cfg["training"]["lr"]),
@@ -156,6 +205,9 @@ def main(argv=None):
     if args.resume:
         start = load_training_state(args.resume, model, optimizer, scaler)
         logger.info(f"Resumed from {args.resume} at epoch {start}")
+    # rank 0's weights and buffers everywhere; bucketed gradient all-reduce hooked into
+    # the backward (side stream) and the optimizer (world > 1)
+    smdist.setup_data_parallel(model, optimizer, world)
     normalizer = ClipNormalizer(device=device)
     logger.info("=" * 50)
     logger.info(f"STARTING PRETRAINING | Total Epochs: {cfg['training']['epochs']}")
@@ -166,6 +218,8 @@ def main(argv=None):
     save_dir = Path(cfg["training"]["save_dir"])
     epochs = cfg["training"]["epochs"]
     for epoch in range(start, epochs + 1):
+        if sampler is not None:
+            sampler.set_epoch(epoch)
         avg, dur = train_one_epoch(model, loader, optimizer, scaler, epoch, device, cfg, writer, logger,
                                    normalizer)
         total = time.time() - t0
@@ -178,10 +232,13 @@ def main(argv=None):
         logger.info(f"    Total Training ETA: {format_time(eta)}")
         logger.info("-" * 30)
         if epoch % 10 == 0:
-            p = save_dir / f"encoder_ep{epoch}.pth"
-            save_checkpoint(model.encoder.state_dict(), p)
-            save_training_state(save_dir / "last_state.pth", model, optimizer, scaler, epoch)
-            logger.info(f"Checkpoint saved to {p}")
+            if rank == 0:
+                p = save_dir / f"encoder_ep{epoch}.pth"
+                save_checkpoint(model.encoder.state_dict(), p)
+                save_training_state(save_dir / "last_state.pth", model, optimizer, scaler, epoch)
+                logger.info(f"Checkpoint saved to {p}")
+            if world > 1:
+                dist.barrier()
     return model
 
 

@@ -17,6 +17,11 @@ Sequence recorded (B=2 clips, T=16 frames, 112x112, 101 classes):
      (updated once per frame call: num_batches_tracked = T);
   2. evaluation forward (train_finetune.py:127-138): model.eval() under no_grad on
      a second clip -> logits, embeddings.
+A second fixture, finetune_ftssl_b2_t2_s112.npz (ft_ssl mode, :198-210: backbone
+trainable), records one fp32 training step's backbone gradients (B=2, T=2, 112x112,
+DropPath 0, model.train()): per parameter the gradient sum, L2 norm and first 8
+values, plus loss and logits -- the T per-frame backward groups summed into each
+backbone gradient.
 Run:  python tests/golden/make_golden_finetune.py
 """
 import os
@@ -97,5 +102,40 @@ def main():
     print(f"wrote {out}: train loss {loss.item():.6f}, eval logits[0,:3] {logits2[0, :3].tolist()}")
 
 
+def ftssl_case():
+    tiny_vit = MG._import_reference()[0]
+    torch.set_num_threads(8)
+    B, T, S, NC = 2, 2, 112, 11
+    model = RefClassifier(tiny_vit, NC, S)
+    apply_rule(model)
+    for m in model.modules():
+        if hasattr(m, "drop_prob"):
+            m.drop_prob = 0.0
+    clip = torch.from_numpy(synthetic_clip(B, T, S, seed=2468))
+    label = torch.tensor([1, 7])
+    model.train()
+    logits = model(clip)
+    loss = nn.CrossEntropyLoss()(logits, label)
+    loss.backward()
+    rec = {"B": B, "T": T, "S": S, "num_classes": NC, "loss": np.float64(loss.item()),
+           "logits": logits.detach().numpy()}
+    names = []
+    for n, p in model.named_parameters():
+        if p.grad is None:
+            continue
+        g = p.grad.detach().double().reshape(-1)
+        names.append(n)
+        rec["gsum/" + n] = np.float64(g.sum())
+        rec["gl2/" + n] = np.float64(g.norm())
+        rec["ghead/" + n] = g[:8].numpy().copy()
+    rec["names"] = np.array(names)
+    out = os.path.join(HERE, "finetune_ftssl_b2_t2_s112.npz")
+    np.savez_compressed(out, **rec)
+    print(f"wrote {out}: loss {loss.item():.6f}, {len(names)} parameters with gradients")
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "ftssl":
+        ftssl_case()
+    else:
+        main()

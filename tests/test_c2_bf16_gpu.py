@@ -377,3 +377,95 @@ def test_bf16_full_c2_step_properties():
         if name.endswith("num_batches_tracked") and ".stages.3." not in name:
             want = 2 if "patch_embed" in name else 4      # stem once per step, stages 0-2 twice
             assert int(b) == want, name
+
+
+# ------------------------------------------------------------------ C3 "ViT-Small", bf16
+def _small_model(cfg, parity=True):
+    from ssl_mae_amd import parity_mode
+    from ssl_mae_amd.init_rule import apply_rule
+    from ssl_mae_amd.mae_vit_adapter import TinyVideoMAE
+    from ssl_mae_amd.tiny_vit import tiny_vit_small_variant
+    m = TinyVideoMAE(tiny_vit_small_variant(img_size=cfg["dataset"]["image_size"]), cfg)
+    apply_rule(m)
+    if parity:
+        parity_mode(m)
+    return m.to(DEV).train()
+
+
+def test_bf16_small_step_vs_reference_golden(golden_dir):
+    """BASELINE config 3's build-defined ViT-Small (TinyViT depths 2,2,12,2 + 8-layer
+    decoder) at its benchmarked precision: one bf16 step against the
+    reference classes' fp32 step (step_small_b2_t2_s32, tests/golden/make_golden.py)
+    and the oracle's fp32 gradients, with test_bf16_step_t8_224's tolerances (loss
+    2 %, gradient cosine > 0.98, gradient norm within 10 %)."""
+    from oracle import mae_oracle as O
+    from ssl_mae_amd.init_rule import param_value, synthetic_clip
+    from ssl_mae_amd.optim import FusedAdamW, GradScaler
+    from ssl_mae_amd.train_ssl_mae import train_step
+    d = np.load(os.path.join(golden_dir, "step_small_b2_t2_s32.npz"))
+    B, T, S, r = int(d["B"]), int(d["T"]), int(d["S"]), float(d["ratio"])
+    cfg = _cfg(B, T, S, r)
+    cfg["model"]["decoder_depth"] = int(d["decoder_depth"])
+    model = _small_model(cfg)
+    assert tuple(model.encoder.depths) == tuple(int(v) for v in d["depths"])
+    opt = FusedAdamW(model.parameters(), lr=5e-4, weight_decay=0.05)
+    clip = torch.from_numpy(synthetic_clip(B, T, S, seed=int(d["clip_seed"]))).to(DEV)
+    torch.manual_seed(42)
+    loss, pred, _ = train_step(model, clip, opt, GradScaler(), cfg["ssl"], bf16=True)
+    torch.cuda.synchronize()
+    gl = float(d["avg_loss"])
+    assert abs(loss.item() - gl) < 0.02 * abs(gl), (loss.item(), gl)
+    ocfg = {"dataset": cfg["dataset"], "ssl": cfg["ssl"],
+            "model": dict(cfg["model"], depths=tuple(int(v) for v in d["depths"]))}
+    P = O.make_params(ocfg, param_value)
+    _, grads = O.train_step(P, None, None, clip.cpu(), torch.from_numpy(d["mask"][0]), ocfg)
+    named = dict(model.named_parameters())
+    n = 0
+    for name, g in grads.items():
+        if g is None:
+            continue
+        ours = named[name]._sm_grad.detach().double().cpu().reshape(-1)
+        ref = g.double().reshape(-1)
+        gs = math.sqrt(float(d["grad_sumsq/" + name]))
+        if gs < 1e-6:
+            continue
+        assert abs(ref.norm().item() / gs - 1) < 2e-3, name       # oracle == reference (fp32)
+        cos = float(torch.dot(ours, ref) / (ours.norm() * ref.norm() + 1e-30))
+        assert cos > 0.98, (name, cos)
+        assert abs(ours.norm().item() / ref.norm().item() - 1) < 0.10, name
+        n += 1
+    assert n > 250
+
+
+def test_bf16_small_256_clip_step_properties():
+    """C3's per-GPU share (256 clips, T=8, 224^2, bf16, dropout/DropPath on; all
+    stages checkpointed as the reference, the Small model's auto policy): finite
+    loss near the Tiny B=1 reference value's range, finite gradients, parameters
+    updated, BN counters advanced as the checkpointed forward + recompute does."""
+    from ssl_mae_amd.init_rule import IMAGENET_MEAN, IMAGENET_STD
+    from ssl_mae_amd.optim import FusedAdamW, GradScaler
+    from ssl_mae_amd.train_ssl_mae import train_step
+    torch.cuda.empty_cache()
+    cfg = _cfg(B_BENCH, T_BENCH, S_BENCH, 0.75)
+    cfg["model"]["decoder_depth"] = 8
+    model = _small_model(cfg, parity=False)
+    opt = FusedAdamW(model.parameters(), lr=5e-4, weight_decay=0.05)
+    g = torch.Generator(device=DEV).manual_seed(4321)
+    mean = torch.tensor(IMAGENET_MEAN, device=DEV).view(1, 3, 1, 1, 1)
+    std = torch.tensor(IMAGENET_STD, device=DEV).view(1, 3, 1, 1, 1)
+    clip = (torch.rand(B_BENCH, 3, T_BENCH, S_BENCH, S_BENCH, generator=g, device=DEV) - mean) / std
+    torch.manual_seed(42)
+    p0 = model.decoder_pred.weight.detach().clone()
+    loss, pred, idx = train_step(model, clip, opt, GradScaler(), cfg["ssl"], bf16=True)
+    flat = model._sm_flat
+    assert torch.isfinite(flat.grad[:flat.used_end]).all()
+    assert math.isfinite(loss.item()) and 0.5 < loss.item() < 3.0, loss.item()
+    assert idx.numel() == B_BENCH * T_BENCH * 588
+    assert pred.shape == (B_BENCH, L_DEC, 192)
+    assert not torch.equal(p0, model.decoder_pred.weight)
+    for name, b in model.named_buffers():
+        if name.endswith("num_batches_tracked") and ".stages.3." not in name:
+            want = 1 if "patch_embed" in name else 2
+            assert int(b) == want, name
+    del model, opt, clip, pred, flat
+    torch.cuda.empty_cache()

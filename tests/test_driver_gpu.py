@@ -64,3 +64,18 @@ def test_main_runs_saves_and_resumes_bit_exact(tmp_path, monkeypatch):
     pb = {k: v.detach().cpu() for k, v in b.state_dict().items()}
     for k in pa:
         assert torch.equal(pa[k], pb[k]), k
+
+
+def test_rng_state_round_trip_device_stream():
+    """The device generator's state (seed AND offset) is saved, so torch device RNG
+    use after a resume continues the stream instead of repeating it from the start."""
+    import torch
+    from ssl_mae_amd.checkpoint import _rng_state, _set_rng_state
+    torch.cuda.manual_seed_all(11)
+    torch.rand(1000, device="cuda")
+    st = _rng_state()
+    a = torch.rand(16, device="cuda").cpu()
+    torch.rand(5000, device="cuda")
+    _set_rng_state(st)
+    b = torch.rand(16, device="cuda").cpu()
+    assert torch.equal(a, b)

@@ -123,3 +123,77 @@ def test_full_finetune_backward_runs_through_encoder():
         assert p.grad is not None and torch.isfinite(p.grad).all(), n
     assert model.backbone.stages[3][1].attn.qkv.weight.grad.abs().sum() > 0
     opt.step()
+
+
+def test_train_mode_droppath_masks_differ_across_frame_calls():
+    """Each per-frame backbone call of a train-mode forward draws its own DropPath
+    masks (the reference's per-call torch RNG draws).  The same frame repeated at
+    every t gives identical per-frame embeddings with DropPath off (control) and
+    different ones with it on."""
+    from ssl_mae_amd.finetune import frame_modes
+    from ssl_mae_amd.functions import Mode
+    from ssl_mae_amd.init_rule import synthetic_clip
+    ms = frame_modes(Mode(True, 1234), 4)
+    assert len({m.seed_base for m in ms}) == 4
+    frame = torch.from_numpy(synthetic_clip(4, 1, 112, seed=5)).to(DEV)
+    clip = frame.expand(4, 3, 4, 112, 112).contiguous()
+    for p_drop in (0.0, 0.5):
+        model = _model(5).train()
+        for mod in model.modules():
+            if hasattr(mod, "drop_prob"):
+                mod.drop_prob = p_drop
+        captured = []
+        orig = model.backbone.embed
+
+        def spy(x, mode, frames=None, _orig=orig):
+            out = _orig(x, mode)
+            captured.append(out[0].detach().float().clone())
+            return out
+        model.backbone.embed = spy
+        with torch.no_grad():
+            model(clip)
+        assert len(captured) == 4
+        diffs = [float((captured[t] - captured[0]).abs().max()) for t in range(1, 4)]
+        if p_drop == 0.0:
+            assert max(diffs) == 0.0, diffs
+        else:
+            assert min(diffs) > 0.0, diffs
+
+
+def test_ft_ssl_backbone_gradients_match_reference(golden_dir):
+    """ft_ssl mode (train_finetune.py:198-210: backbone trainable), fp32, DropPath 0:
+    one training step's gradient of EVERY backbone parameter -- the sum of the T
+    per-frame fused backward groups written into the flat gradient buffer -- against
+    the reference's TinyViT run (tests/golden/make_golden_finetune.py ftssl).  Per
+    parameter: L2 norm within 1e-3 relative, sum and first 8 values within 1e-3 of
+    the reference value plus 1e-3 of the parameter's gradient RMS (cancellation)."""
+    from ssl_mae_amd.init_rule import synthetic_clip
+    d = np.load(os.path.join(golden_dir, "finetune_ftssl_b2_t2_s112.npz"))
+    B, T, S, NC = int(d["B"]), int(d["T"]), int(d["S"]), int(d["num_classes"])
+    model = _model(NC).train()
+    clip = torch.from_numpy(synthetic_clip(B, T, S, seed=2468)).to(DEV)
+    logits = model(clip)
+    loss = torch.nn.CrossEntropyLoss()(logits, torch.tensor([1, 7], device=DEV))
+    loss.backward()
+    ok, e = _close(logits.detach().cpu().numpy(), d["logits"], 1e-3, 1e-3)
+    assert ok, ("logits", e)
+    assert abs(loss.item() - float(d["loss"])) < 1e-3 * abs(float(d["loss"]))
+    params = dict(model.named_parameters())
+    names = [str(n) for n in d["names"]]
+    assert sum(n.startswith("backbone.") for n in names) > 150
+    bad = []
+    for n in names:
+        g = params[n].grad
+        assert g is not None, n
+        g = g.detach().double().reshape(-1).cpu()
+        l2, ref_l2 = float(g.norm()), float(d["gl2/" + n])
+        rms = ref_l2 / max(1, g.numel()) ** 0.5
+        if abs(l2 - ref_l2) > 1e-3 * ref_l2 + 1e-9:
+            bad.append((n, "l2", l2, ref_l2))
+        if abs(float(g.sum()) - float(d["gsum/" + n])) > 1e-3 * abs(float(d["gsum/" + n])) + 1e-3 * rms * g.numel() ** 0.5:
+            bad.append((n, "sum", float(g.sum()), float(d["gsum/" + n])))
+        h = g[:8].numpy()
+        ref_h = d["ghead/" + n]
+        if np.any(np.abs(h - ref_h) > 1e-3 * np.abs(ref_h) + 1e-3 * rms):
+            bad.append((n, "head", float(np.max(np.abs(h - ref_h))), rms))
+    assert not bad, bad[:10]
