@@ -15,6 +15,19 @@ def timeit(fn, iters=5):
     return s.elapsed_time(e) / iters
 
 
+# HBM calibration: write-only (fill) and copy of a 4.9 GB bf16 tensor (fc1's output size)
+big = torch.empty(1605632 * 1536, dtype=torch.bfloat16, device="cuda")
+nb = big.numel() * 2
+t = timeit(lambda: big.fill_(1.0))
+print(f"fill (write only) {nb / 1e9:.2f} GB: {t:.3f} ms = {nb / t / 1e6:.0f} GB/s", flush=True)
+src = torch.empty_like(big)
+t = timeit(lambda: big.copy_(src))
+print(f"copy {nb / 1e9:.2f} GB each way: {t:.3f} ms = {2 * nb / t / 1e6:.0f} GB/s (read+write)", flush=True)
+t = timeit(lambda: src.sum())
+print(f"sum (read only) {nb / 1e9:.2f} GB: {t:.3f} ms = {nb / t / 1e6:.0f} GB/s", flush=True)
+del big, src
+torch.cuda.empty_cache()
+
 for name, M, N, Kd in [("fc1", 1605632, 1536, 384), ("fc2", 1605632, 384, 1536), ("qkv", 1605632, 1152, 384),
                        ("s0exp", 6422528, 384, 96), ("s0proj", 6422528, 96, 384)]:
     x = torch.randn(M, Kd, device="cuda").to(torch.bfloat16)

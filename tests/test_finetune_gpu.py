@@ -182,11 +182,18 @@ def test_ft_ssl_backbone_gradients_match_reference(golden_dir):
     names = [str(n) for n in d["names"]]
     assert sum(n.startswith("backbone.") for n in names) > 150
     bad = []
+    top = max(float(d["gl2/" + n]) for n in names)
     for n in names:
         g = params[n].grad
         assert g is not None, n
         g = g.detach().double().reshape(-1).cpu()
         l2, ref_l2 = float(g.norm()), float(d["gl2/" + n])
+        if ref_l2 < 1e-5 * top:
+            # analytically ~zero (a bias feeding a train-mode BatchNorm): rounding noise
+            # on both sides; only its size is checked
+            if l2 > 1e-4 * top:
+                bad.append((n, "noise", l2, top))
+            continue
         rms = ref_l2 / max(1, g.numel()) ** 0.5
         if abs(l2 - ref_l2) > 1e-3 * ref_l2 + 1e-9:
             bad.append((n, "l2", l2, ref_l2))
