@@ -47,8 +47,34 @@ def cls(ins):
     return "s"
 
 
+def loop_census(lines, start, end):
+    """Instruction classes summed over every block of the kernel that lies in a loop
+    (label comment 'in Loop:' or 'Loop Header:'), by innermost loop header."""
+    loops, cur = {}, None
+    for ln in lines[start:end]:
+        s = ln.strip()
+        m = re.match(r"^(\.LBB\d+_\d+):.*(?:Header=(\S+)|Loop Header)", s)
+        if re.match(r"^\.LBB\d+_\d+:", s):
+            cur = None
+            if m:
+                cur = m.group(2) or m.group(1).lstrip(".")
+                loops.setdefault(cur, [])
+            continue
+        if cur and s and not s.startswith((";", ".", "//")):
+            loops[cur].append(cls(s))
+    return loops
+
+
 def main():
     path, kern = sys.argv[1], sys.argv[2]
+    if "--loops" in sys.argv:
+        lines = open(path).read().split("\n")
+        start = next(i for i, ln in enumerate(lines) if ln.startswith("_Z") and kern in ln and ln.split(";")[0].rstrip().endswith(":"))
+        end = next(i for i in range(start + 1, len(lines)) if lines[i].strip().startswith(".Lfunc_end"))
+        for hdr, seq in loop_census(lines, start, end).items():
+            seq = "".join(seq)
+            print(kern, hdr, len(seq), {c: seq.count(c) for c in "MVTDSWNBGs"})
+        return
     lines = open(path).read().split("\n")
     start = next(i for i, ln in enumerate(lines) if ln.startswith("_Z") and kern in ln and ln.split(";")[0].rstrip().endswith(":"))
     end = next(i for i in range(start + 1, len(lines)) if lines[i].strip().startswith(".Lfunc_end"))

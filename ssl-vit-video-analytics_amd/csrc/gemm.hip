@@ -58,6 +58,9 @@ struct GemmArgs {
   // BatchNorm statistics of the bf16 output (IMP 8, sm_linear_bn_stats): per-wave column sums
   // and sums of squares of the stored values, [m-tile x waves along M][2][N]
   float* stat_part;
+  // split-K reduce only: store C transposed, C[col * ldc + row] (a weight gradient computed
+  // as dW^T = x^T dy, sm_linear_dw_bias)
+  int ctrans;
 };
 
 template <typename TC>
@@ -69,7 +72,7 @@ SM_DEV void epilogue_store(const GemmArgs& g, int64_t row, int col, float acc, i
   float v = g.alpha * acc;
   if (g.bias) v += g.bias[col];
   TC* C = (TC*)g.C;
-  const int64_t idx = row * g.ldc + col;
+  const int64_t idx = g.ctrans ? (int64_t)col * g.ldc + row : row * g.ldc + col;
   if (g.epi & 2) v = (float)(__bf16)v;   // autocast: the Linear output is bf16 before the fp32 add
   if (g.epi & 4) v *= gelu_grad(to_f<TC>(((const TC*)g.aux)[idx]));
   if (g.epi & 1) {
@@ -1300,9 +1303,35 @@ extern "C" int sm_gemm(int ab_dtype, int c_dtype, int a_layout, int b_layout, in
 // Weight and bias gradients of y = x W^T + b in one pass over dy: dW[nout][nin] (+)=
 // dy^T x and db[nout] += column sums of dy (reference: the Linear / 1x1-conv
 // backward autograd runs as two ops, a GEMM and a sum over rows).  bf16 operands.
+extern "C" int64_t sm_colsum_workspace_bytes(int64_t M, int C);
+extern "C" int sm_colsum(int dtype, int64_t M, int C, const void* x, float* out, int accumulate, void* ws,
+                         int64_t ws_bytes, hipStream_t st);
+
+namespace {
+// Output rows x columns the bf16 v2 kernel computes for an M x N product (tile quantisation).
+int64_t tiled_area(int M, int N) {
+  const int bm = variant_bm(gemm_variant(M, N, 0));
+  return (int64_t)((M + bm - 1) / bm) * bm * ((N + 127) / 128) * 128;
+}
+// dW = dy^T x computed transposed (dW^T = x^T dy: M = nin, N = nout) when that tiles the
+// output with less waste and still splits K (the transposed store lives in the split-K
+// reduce).  fc2's [384][1536] weight gradient: two 256-row m-tiles, one half empty, vs six
+// exact ones -- the shape of fc1's [1536][384] gradient, which ran 2x faster.
+// Only when the transposed tiling is exact: [576][192] tiles smaller transposed (192 rows on
+// a 256-row tile) yet ran 3.45 -> 4.40 ms (profiles/r03g_dw_ab.txt).
+bool dw_transposed(int rows, int nout, int nin) {
+  return tiled_area(nin, nout) == (int64_t)nin * nout && tiled_area(nout, nin) * 10 > (int64_t)nout * nin * 11 &&
+         choose_splits(nin, nout, rows, true) > 1;
+}
+}  // namespace
+
 extern "C" int64_t sm_linear_dw_bias_workspace_bytes(int rows, int nout, int nin) {
   const int s = choose_splits(nout, nin, rows, true);
-  return (s > 1 ? (int64_t)s * nout * nin * 4 : 0) + (int64_t)s * nout * 4 + 256;
+  const int64_t plain = (s > 1 ? (int64_t)s * nout * nin * 4 : 0) + (int64_t)s * nout * 4 + 256;
+  if (!dw_transposed(rows, nout, nin)) return plain;
+  const int st = choose_splits(nin, nout, rows, true);
+  const int64_t tr = (int64_t)st * nout * nin * 4 + 256 + sm_colsum_workspace_bytes(rows, nout);
+  return plain > tr ? plain : tr;
 }
 
 // fc2's weight gradient dW[nout][nin] (+)= dy^T dropout(GELU(pre)), db += colsum(dy),
@@ -1494,6 +1523,29 @@ extern "C" int sm_linear_dw_bias(int rows, int nout, int nin, const void* dy, co
   if (nout <= 0 || nin <= 0) return 0;
   if (ws_bytes < sm_linear_dw_bias_workspace_bytes(rows, nout, nin)) return -4;
   if (gemm_variant(nout, nin, rows) == 1 || nout % 8 || nin % 8) return -2;   // the row sums live in the v2 kernel
+  if (dw_transposed(rows, nout, nin)) {
+    // dW^T[nin][nout] = x^T dy (split-K slabs), reduced into dW[nout][nin] through the
+    // transposed store; db = column sums of dy by the colsum kernel (the fused row sums
+    // follow the A operand, which is x here)
+    const int s = choose_splits(nin, nout, rows, true);
+    const int64_t gbytes = (int64_t)s * nout * nin * 4;
+    GemmArgs g{};
+    g.M = nin; g.N = nout; g.K = rows; g.A = x; g.lda = nin; g.B = dy; g.ldb = nout; g.C = dW; g.ldc = nin;
+    g.alpha = 1.f; g.beta = accumulate ? 1.f : 0.f; g.rows_per_group = 1; g.ctrans = 1;
+    int chunk = (rows + s - 1) / s;
+    chunk = (chunk + BKT - 1) / BKT * BKT;
+    const int splits = (rows + chunk - 1) / chunk;
+    g.k_begin = 0; g.k_chunk = chunk; g.partial = (float*)ws;
+    launch_bf16<false, false, float, true>(g, splits, stream);
+    SM_CHECK_LAUNCH();
+    const int64_t total = (int64_t)nout * nin;
+    int blocks = (int)((total + 255) / 256);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(splitk_reduce_kernel<float>, dim3(blocks), dim3(256), 0, stream, g, splits);
+    SM_CHECK_LAUNCH();
+    void* cws = (void*)(((uintptr_t)ws + gbytes + 255) & ~(uintptr_t)255);
+    return sm_colsum(SM_BF16, rows, nout, dy, db, 1, cws, sm_colsum_workspace_bytes(rows, nout), stream);
+  }
   const int s = choose_splits(nout, nin, rows, true);
   const int64_t gbytes = s > 1 ? (int64_t)s * nout * nin * 4 : 0;
   float* colsum = (float*)(((uintptr_t)ws + gbytes + 15) & ~(uintptr_t)15);
