@@ -53,6 +53,12 @@ int sm_linear_dw_bias(int rows, int nout, int nin, const void* dy, const void* x
  * tiny_vit.py:74-84, the decoder feed-forward).  Bit-identical to sm_gelu_fwd followed by
  * sm_linear_dw_bias without the recompute pass; workspace as
  * sm_linear_dw_bias_workspace_bytes. */
+/* The fc2 data gradient through dropout(GELU(pre)) with the fc2 weight gradient's operand
+ * as a side output (Mlp tiny_vit.py:74-84, decoder FF mae_vit_adapter.py:40-48): dx = (dy w)
+ * * keep / (1 - p) * GELU'(pre) and h = bf16(GELU(pre) * keep / (1 - p)) (= sm_gelu_fwd(pre))
+ * from one epilogue.  dy [M][N], w [N][K], pre / dx / h [M][K] bf16; N, K % 8 == 0. */
+int sm_linear_dx_gelu(int M, int N, int K, const void* dy, const void* w, const void* pre, void* dx, void* h,
+                      float drop_p, uint64_t seed, hipStream_t stream);
 int sm_linear_dw_bias_gelu(int rows, int nout, int nin, const void* dy, const void* pre, float drop_p,
                            uint64_t seed, float* dW, float* db, int accumulate, void* ws, int64_t ws_bytes,
                            hipStream_t stream);
@@ -178,6 +184,12 @@ int sm_conv_wunpack_add(const float* packed, float* grad, int Cout, int Cin, int
  * fwd: y = conv(x); dgrad: dx = conv^T(dy); wgrad: dw[Cout][9*Cin] (+)= fp32 weight
  * gradient (unpack with sm_conv_wunpack_add order 1). */
 int sm_conv3x3_fwd(const void* x, const void* wpack, void* y, int F, int H, int W, int Cin, int Cout, hipStream_t st);
+/* conv fwd + the train-mode BatchNorm statistics of y (tiny_vit.py:69-70, the stem's conv2
+ * -> BN) from the GEMM epilogue, as sm_linear_bn_stats (workspace =
+ * sm_linear_bn_stats_workspace_bytes(F*H*W, Cout)); replaces sm_conv3x3_fwd + sm_bn_stats. */
+int sm_conv3x3_fwd_bn_stats(const void* x, const void* wpack, void* y, int F, int H, int W, int Cin, int Cout,
+                            float* mean, float* rstd, float* run_mean, float* run_var, int64_t* num_batches_tracked,
+                            float momentum, float eps, int updates, void* ws, int64_t ws_bytes, hipStream_t st);
 int sm_conv3x3_dgrad(const void* dy, const void* wpack_t, void* dx, int F, int H, int W, int Cin, int Cout,
                      hipStream_t st);
 int64_t sm_conv3x3_wgrad_workspace_bytes(int F, int H, int W, int Cin, int Cout);

@@ -61,6 +61,9 @@ struct GemmArgs {
   // split-K reduce only: store C transposed, C[col * ldc + row] (a weight gradient computed
   // as dW^T = x^T dy, sm_linear_dw_bias)
   int ctrans;
+  // IMP 9 only (sm_linear_dx_gelu): side output of the GELU input aux, aux_out = bf16(GELU(aux)
+  // * dropout keep / (1 - p)) = sm_gelu_fwd(aux) -- the fc2 weight gradient's operand
+  void* aux_out;
 };
 
 template <typename TC>
@@ -374,6 +377,7 @@ SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x
           if (g.epi & 2) v[e] = (float)(__bf16)v[e];
         }
         const int64_t idx = row * g.ldc + col;
+        float hg[8];       // AUXS side output: GELU(pre) (x keep / (1 - p) below)
         if (g.epi & 4) {   // GELU backward: the saved pre-activation run of this (row, cols)
           float pre[8];
           if (AUXS && sizeof(TC) == 2 && stage) {
@@ -384,6 +388,10 @@ SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x
           }
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] *= gelu_grad(pre[e]);
+          if (AUXS && g.aux_out) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) hg[e] = gelu_f(pre[e]);
+          }
         }
         if (g.epi & 1) {
           if (g.aux) {
@@ -398,8 +406,16 @@ SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x
           for (int e4 = 0; e4 < 8; e4 += 4) {
             const uint32_t hv = drop_hash(rb, (uint32_t)(col + e4));   // col % 8 == 0
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e4 + e] *= ((hv >> (8 * e)) & 0xFFu) >= thr ? ks : 0.f;
+            for (int e = 0; e < 4; ++e) {
+              const float m = ((hv >> (8 * e)) & 0xFFu) >= thr ? ks : 0.f;
+              v[e4 + e] *= m;
+              if (AUXS && g.aux_out) hg[e4 + e] *= m;
+            }
           }
+        }
+        if (AUXS && g.aux_out) {   // over this lane's own pre run in stage region 1 (read above)
+          if (stage && sizeof(TC) == 2) stage_put<TC>(rs_, 1, j, p, h, l, hg);
+          else store8((TC*)g.aux_out + idx, hg);
         }
         if (g.row_scale) {
 #pragma unroll
@@ -425,6 +441,7 @@ SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x
       const int64_t r0 = m0 + wm + 32 * i;
       const int c0 = n0 + wn;
       if (g.aux && (g.epi & 1)) rs_.flush<TC>(1, (TC*)g.aux, g.ldc, r0, c0, g.M, g.N, l);
+      if (AUXS && g.aux_out) rs_.flush<TC>(1, (TC*)g.aux_out, g.ldc, r0, c0, g.M, g.N, l);
       if constexpr (STATS) rs_.flush<TC, true>(0, (TC*)g.C, g.ldc, r0, c0, g.M, g.N, l, st1, st2);
       else rs_.flush<TC>(0, (TC*)g.C, g.ldc, r0, c0, g.M, g.N, l);
     }
@@ -787,7 +804,8 @@ struct XformColsB {
 
 // IMP: 0 plain operands (8: plus the output's BatchNorm statistics in the epilogue,
 // sm_linear_bn_stats; 9: the GELU-backward pre-activation staged through LDS by whole
-// lines); 1 A is the implicit im2col of a conv (ConvRowsA);
+// lines); 1 A is the implicit im2col of a conv (ConvRowsA; 10: plus the output's
+// BatchNorm statistics as IMP 8, sm_conv3x3_fwd_bn_stats);
 // 2 B is (ConvColsB); 5 / 7 B is formed on load (XformColsB); 6 A (K-major) is the
 // SE output formed on load (below).
 // (IMP 5: the activation's registers do not fit beside the staging set at 4 waves /
@@ -835,7 +853,7 @@ __global__ __launch_bounds__(BMV * 2, (BMV == 256 && IMP != 5 && IMP != 6 && IMP
   ConvRowsA<BMV, NT> cla;
   ConvColsB<BNV, NT> clb;
   XformColsB<BNV, NT, IMP> xlb;
-  if constexpr (IMP == 1) cla.init(g, m0, kb);
+  if constexpr (IMP == 1 || IMP == 10) cla.init(g, m0, kb);
   else tla.init(g.lda, g.M - m0);
   if constexpr (IMP == 2) clb.init(g, n0, kb);
   else if constexpr (XB) xlb.init(g, n0);
@@ -849,7 +867,7 @@ __global__ __launch_bounds__(BMV * 2, (BMV == 256 && IMP != 5 && IMP != 6 && IMP
   // (W + 1)-pixel halo; B's advances with K (its rows are pixels)
   const int64_t cbase = -(int64_t)(g.cW + 1) * g.cC;
   auto load_a = [&](int k0, uint4 (&r)[TileLoader<BMV, NT, AK>::CH]) {
-    if constexpr (IMP == 1) cla.load(panel_rsrc(A, (int64_t)m0 * g.cC + cbase), g, ke, r);
+    if constexpr (IMP == 1 || IMP == 10) cla.load(panel_rsrc(A, (int64_t)m0 * g.cC + cbase), g, ke, r);
     else tla.load(panel_rsrc(A, abase + k0 * astep), ke - k0, r);
   };
   auto load_b = [&](int k0, uint4 (&r)[TileLoader<BNV, NT, BK>::CH]) {
@@ -887,7 +905,7 @@ __global__ __launch_bounds__(BMV * 2, (BMV == 256 && IMP != 5 && IMP != 6 && IMP
         for (int j = 0; j < 8; ++j) cs8[j] += (float)v[j];
       }
     }
-    if constexpr (IMP == 1) {
+    if constexpr (IMP == 1 || IMP == 10) {
       cla.store(la, ra);
     } else if constexpr (IMP == 6) {
       // h3 = bf16(bf16(GELU(a2 sc + sh)) * gate), exactly as se_apply_kernel stores it;
@@ -949,7 +967,7 @@ __global__ __launch_bounds__(BMV * 2, (BMV == 256 && IMP != 5 && IMP != 6 && IMP
     }
     __syncthreads();
   }
-  gemm_epilogue<TC, VEC, 2, 2, IMP == 8, IMP == 9>(g, acc, m0, n0, wm, wn, l, zs, lds + w * 8192);
+  gemm_epilogue<TC, VEC, 2, 2, IMP == 8 || IMP == 10, IMP == 9>(g, acc, m0, n0, wm, wn, l, zs, lds + w * 8192);
 }
 
 // ============================================================ f32 MFMA kernel
@@ -1144,7 +1162,7 @@ void launch_conv(const GemmArgs& g, int splits, hipStream_t st) {
   const int v = gemm_variant(g.M, g.N, 0) == 2 ? 2 : 3;
   const int bm = variant_bm(v);
   dim3 grid(((g.N + 127) / 128) * ((g.M + bm - 1) / bm) * splits);
-  constexpr bool AK = IMP == 1, BK = IMP == 1;
+  constexpr bool AK = IMP == 1 || IMP == 10, BK = AK;
   if (v == 2) hipLaunchKernelGGL((gemm_bf16_v2<AK, BK, TC, true, 256, IMP>), grid, dim3(512), 0, st, g);
   else hipLaunchKernelGGL((gemm_bf16_v2<AK, BK, TC, true, 128, IMP>), grid, dim3(256), 0, st, g);
 }
@@ -1288,6 +1306,28 @@ static int gemm_run(int ab_dtype, int c_dtype, int a_layout, int b_layout, int M
     colred(colsum, K > 0 ? splits : 0, M, nullptr, colsum_out, 1, stream);
     SM_CHECK_LAUNCH();
   }
+  return 0;
+}
+
+// fc2 data gradient through dropout(GELU(pre)) plus the fc2 weight gradient's operand
+// (tiny_vit.py:74-84 Mlp / mae_vit_adapter.py:40-48 decoder FF backward): dx = (dy w) *
+// keep / (1 - p) * GELU'(pre) and h = bf16(GELU(pre) * keep / (1 - p)) (bit-identical to
+// sm_gelu_fwd(pre)) from one epilogue that reads pre once -- no recompute pass of h.
+// dy [M][N], w [N][K], pre / dx / h [M][K] bf16; K % 8 == 0, N % 8 == 0.
+extern "C" int sm_linear_dx_gelu(int M, int N, int K, const void* dy, const void* w, const void* pre, void* dx,
+                                 void* h, float drop_p, uint64_t seed, hipStream_t stream) {
+  if (M <= 0 || K <= 0) return 0;
+  if (N <= 0 || N % 8 || K % 8 || (((uintptr_t)dy | (uintptr_t)w | (uintptr_t)pre | (uintptr_t)dx | (uintptr_t)h) & 15))
+    return -2;
+  GemmArgs g{};
+  g.M = M; g.N = K; g.K = N; g.A = dy; g.lda = N; g.B = w; g.ldb = K; g.C = dx; g.ldc = K;
+  g.alpha = 1.f; g.beta = 0.f; g.epi = 4; g.aux = const_cast<void*>(pre); g.aux_out = h;
+  g.drop_p = drop_p; g.seed = seed; g.rows_per_group = 1; g.k_begin = 0; g.k_chunk = N;
+  const int v = gemm_variant(g.M, g.N, g.K);
+  const int tiles = ((g.N + 127) / 128) * ((g.M + variant_bm(v) - 1) / variant_bm(v));
+  if (v == 2) hipLaunchKernelGGL((gemm_bf16_v2<true, false, __bf16, true, 256, 9>), dim3(tiles), dim3(512), 0, stream, g);
+  else hipLaunchKernelGGL((gemm_bf16_v2<true, false, __bf16, true, 128, 9>), dim3(tiles), dim3(256), 0, stream, g);
+  SM_CHECK_LAUNCH();
   return 0;
 }
 
@@ -1473,6 +1513,32 @@ extern "C" int sm_linear_bn_stats(int M, int N, int K, const void* x, const void
   SM_CHECK_LAUNCH();
   return sm_bn_stats_from_partials(part2, nch, N, M, mean, rstd, run_mean, run_var, num_batches_tracked, momentum,
                                    eps, updates, fin, 2 * (int64_t)N * 8, stream);
+}
+
+// stem conv2 forward + the output's train-mode BatchNorm statistics from the GEMM epilogue (as
+// sm_linear_bn_stats: no read pass of y for the statistics); the stem's conv2 -> BN2
+extern "C" int sm_conv3x3_fwd_bn_stats(const void* x, const void* wpack, void* y, int F, int H, int W, int Cin,
+                                       int Cout, float* mean, float* rstd, float* run_mean, float* run_var,
+                                       int64_t* num_batches_tracked, float momentum, float eps, int updates, void* ws,
+                                       int64_t ws_bytes, hipStream_t st) {
+  const int64_t P = (int64_t)F * H * W;
+  if (!conv_shape_ok(P, H, W, Cin, Cout, x, wpack, y)) return -2;
+  if (ws_bytes < sm_linear_bn_stats_workspace_bytes((int)P, Cout)) return -4;
+  const int64_t nparts = (P + 63) / 64;
+  float* part = (float*)ws;
+  float* part2 = part + nparts * 2 * Cout;
+  void* fin = (void*)(((uintptr_t)(part2 + (int64_t)LBS_CHUNKS * 2 * Cout) + 15) & ~(uintptr_t)15);
+  GemmArgs g = conv_args((int)P, Cout, 9 * Cin, x, Cin, wpack, 9 * Cin, y, Cout, H, W, Cin, 0);
+  g.stat_part = part;
+  launch_conv<10, __bf16>(g, 1, st);
+  SM_CHECK_LAUNCH();
+  const int64_t chunk = (nparts + LBS_CHUNKS - 1) / LBS_CHUNKS;
+  const int nch = (int)((nparts + chunk - 1) / chunk);
+  hipLaunchKernelGGL(rowchunk_sum_kernel, dim3((2 * Cout + 31) / 32, nch), dim3(256), 0, st, part, nparts, 2 * Cout,
+                     chunk, part2);
+  SM_CHECK_LAUNCH();
+  return sm_bn_stats_from_partials(part2, nch, Cout, P, mean, rstd, run_mean, run_var, num_batches_tracked, momentum,
+                                   eps, updates, fin, 2 * (int64_t)Cout * 8, st);
 }
 
 extern "C" int64_t sm_linear_dw_se_workspace_bytes(int rows, int nout, int nin) {

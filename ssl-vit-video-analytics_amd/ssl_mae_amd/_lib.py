@@ -52,6 +52,7 @@ _SIGS = {
     "sm_add": (_c_i32, [_c_i32, _c_i32, _c_i64, _c_p, _c_p, _c_p, _c_p]),
     "sm_cast": (_c_i32, [_c_i32, _c_i32, _c_i64, _c_p, _c_p, _c_p]),
     "sm_fill": (_c_i32, [_c_p, _c_i64, _c_f32, _c_p]),
+    "sm_linear_dx_gelu": (_c_i32, [_c_i32] * 3 + [_c_p] * 5 + [_c_f32, _c_u64, _c_p]),
     "sm_gelu_fwd": (_c_i32, [_c_i32, _c_i64, _c_i32, _c_p, _c_p, _c_f32, _c_u64, _c_p]),
     "sm_linear_dw_bias_workspace_bytes": (_c_i64, [_c_i32, _c_i32, _c_i32]),
     "sm_linear_dw_bias": (_c_i32, [_c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_i64, _c_p]),
@@ -73,6 +74,8 @@ _SIGS = {
     "sm_col2im3": (_c_i32, [_c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p]),
     "sm_conv_wpack": (_c_i32, [_c_i32, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p]),
     "sm_conv3x3_fwd": (_c_i32, [_c_p, _c_p, _c_p] + [_c_i32] * 5 + [_c_p]),
+    "sm_conv3x3_fwd_bn_stats": (_c_i32, [_c_p, _c_p, _c_p] + [_c_i32] * 5 + [_c_p] * 5
+                                + [_c_f32, _c_f32, _c_i32, _c_p, _c_i64, _c_p]),
     "sm_conv3x3_dgrad": (_c_i32, [_c_p, _c_p, _c_p] + [_c_i32] * 5 + [_c_p]),
     "sm_conv3x3_wgrad_workspace_bytes": (_c_i64, [_c_i32] * 5),
     "sm_conv3x3_wgrad": (_c_i32, [_c_p, _c_p, _c_p] + [_c_i32] * 6 + [_c_p, _c_i64, _c_p]),

@@ -113,14 +113,20 @@ class StemFn(torch.autograd.Function):
             del col1
             h1, m1, r1 = _bn_forward(a1, st.bn1, gelu=True)
         w2p = K.conv_wpack(w2.detach(), 432, 1, act)
-        if mode.bf16:       # conv2 as a GEMM over the implicit im2col of h1 (no 9x buffer)
-            a2 = K.conv3x3_fwd(h1, w2p, Fr, Ho, Wo, 48, 96)
-        else:               # fp32 parity path: explicit im2col + exact-fp32 GEMM
-            col2 = K.im2col3(h1, Fr, Ho, Wo, 48, 1)
-            a2 = K.linear(col2, w2p)
-            del col2
-        del h1
-        y, m2, r2 = _bn_forward(a2, st.bn2, gelu=False)
+        if mode.bf16 and st.bn2.training:   # conv2 as a GEMM over the implicit im2col of h1
+            # (no 9x buffer) with BN2's statistics from its epilogue (no read pass of a2)
+            a2, m2, r2 = K.conv3x3_fwd_bn_stats(h1, w2p, Fr, Ho, Wo, 48, 96, st.bn2)
+            del h1
+            y = K.bn_apply(a2, m2, r2, g2.detach(), b2.detach(), gelu=False)
+        else:
+            if mode.bf16:
+                a2 = K.conv3x3_fwd(h1, w2p, Fr, Ho, Wo, 48, 96)
+            else:           # fp32 parity path: explicit im2col + exact-fp32 GEMM
+                col2 = K.im2col3(h1, Fr, Ho, Wo, 48, 1)
+                a2 = K.linear(col2, w2p)
+                del col2
+            del h1
+            y, m2, r2 = _bn_forward(a2, st.bn2, gelu=False)
         ctx.st = st
         ctx.geom = (Fr, Ho, Wo)
         ctx.params = (w1, g1, b1, w2, g2, b2)
@@ -360,15 +366,21 @@ class BlockFn(torch.autograd.Function):
             db = dout if dout.dtype == act else K.cast(dout, act)       # grad of the bf16 branch
             if regs2:
                 db = K.dropout_bwd(db, st.drop2, st.seed2, st.dp2, L)
-        if rb:   # fc2 weight gradient of dropout(GELU(hpre)) (kernels.linear_dw_bias picks the form)
+        # dL/dhpre straight from the fc2 data-gradient GEMM's epilogue (keep mask and
+        # GELU' applied there: no dh round trip, no gelu_bwd pass)
+        if rb and db.shape[1] <= 256:
+            # one-m-tile fc2 weight gradient: dropout(GELU(hpre)) formed in its operand loads
             K.linear_dw_bias(db, hpre, G(w2), G(b2), gelu=(st.drop_ff, st.seed_ff))
+            dhpre = K.linear_dx(db, W(w2, mode), gelu_pre=hpre, drop_p=st.drop_ff, seed=st.seed_ff)
+        elif rb:   # h = dropout(GELU(hpre)) as a side output of the dX epilogue (hpre read once)
+            dhpre, h = K.linear_dx_gelu(db, W(w2, mode), hpre, st.drop_ff, st.seed_ff)
+            K.linear_dw_bias(db, h, G(w2), G(b2))
+            del h
         else:
             h = K.gelu(hpre, st.drop_ff, st.seed_ff)
             K.linear_dw_bias(db, h, G(w2), G(b2))
             del h
-        # dL/dhpre straight from the fc2 data-gradient GEMM's epilogue (keep mask and
-        # GELU' applied there: no dh round trip, no gelu_bwd pass)
-        dhpre = K.linear_dx(db, W(w2, mode), gelu_pre=hpre, drop_p=st.drop_ff, seed=st.seed_ff)
+            dhpre = K.linear_dx(db, W(w2, mode), gelu_pre=hpre, drop_p=st.drop_ff, seed=st.seed_ff)
         del db
         ln2 = K.layernorm(x2, ln2w.detach(), ln2b.detach(), out_dtype=act, eps=st.eps)[0]
         K.linear_dw_bias(dhpre, ln2, G(w1), G(b1))

@@ -69,6 +69,22 @@ def linear_dx(dy, w, out_dtype=None, residual=None, gelu_pre=None, drop_p=0.0, s
     return out
 
 
+def linear_dx_gelu(dy, w, pre, drop_p=0.0, seed=0):
+    """(dL/dpre, h) of y = dropout(GELU(pre)) @ w^T: dL/dpre = linear_dx(dy, w, gelu_pre=pre)
+    and h = gelu(pre, drop_p, seed) (the fc2 weight gradient's operand) from one GEMM
+    epilogue (sm_linear_dx_gelu): pre is read once, no recompute pass.  bf16 only."""
+    _chk(dy, w, pre)
+    M, N = dy.shape
+    K = w.shape[1]
+    if (dy.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or pre.dtype != torch.bfloat16
+            or tuple(pre.shape) != (M, K) or w.shape[0] != N):
+        raise _lib.KernelError("linear_dx_gelu: bf16 dy [M,N], w [N,K], pre [M,K]")
+    dx = torch.empty((M, K), dtype=torch.bfloat16, device=dy.device)
+    h = torch.empty_like(dx)
+    call("sm_linear_dx_gelu", M, N, K, ptr(dy), ptr(w), ptr(pre), ptr(dx), ptr(h), float(drop_p), int(seed), stream())
+    return dx, h
+
+
 def linear_dw(dy, x, grad_sink, accumulate=True):
     """grad_sink[N,K] (+)= dy^T @ x   (fp32 sink; reduction over the M token rows)."""
     M, N = dy.shape
@@ -385,6 +401,26 @@ def conv3x3_fwd(x, wpack, F, H, W, Cin, Cout):
     y = torch.empty((F * H * W, Cout), dtype=torch.bfloat16, device=x.device)
     call("sm_conv3x3_fwd", ptr(x), ptr(wpack), ptr(y), F, H, W, Cin, Cout, stream())
     return y
+
+
+def conv3x3_fwd_bn_stats(x, wpack, F, H, W, Cin, Cout, running_mean=None, running_var=None, momentum=0.1,
+                         eps=1e-5, updates=1, num_batches=None):
+    """conv3x3_fwd plus the train-mode BatchNorm statistics of y from the GEMM epilogue
+    (sm_conv3x3_fwd_bn_stats; = conv3x3_fwd + bn_stats without the read pass of y).
+    Returns (y, mean, rstd)."""
+    _chk(x, wpack)
+    _conv_chk(x, Cin)
+    _conv_chk(wpack, 9 * Cin)
+    P = F * H * W
+    y = torch.empty((P, Cout), dtype=torch.bfloat16, device=x.device)
+    mean = torch.empty(Cout, dtype=torch.float32, device=x.device)
+    rstd = torch.empty(Cout, dtype=torch.float32, device=x.device)
+    nbytes = query("sm_linear_bn_stats_workspace_bytes", P, Cout)
+    ws = _ws(nbytes, x.device)
+    call("sm_conv3x3_fwd_bn_stats", ptr(x), ptr(wpack), ptr(y), F, H, W, Cin, Cout, ptr(mean), ptr(rstd),
+         ptr(running_mean), ptr(running_var), ptr(num_batches), float(momentum), float(eps), int(updates), ptr(ws),
+         nbytes, stream())
+    return y, mean, rstd
 
 
 def conv3x3_dgrad(dy, wpack_t, F, H, W, Cin, Cout):

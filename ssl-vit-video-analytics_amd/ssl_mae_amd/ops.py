@@ -138,6 +138,21 @@ def linear_dx(dy, w, out_dtype=None, residual=None, gelu_pre=None, drop_p=0.0, s
     return torch.ops.ssl_mae.linear_dx(dy, w, out_dtype, residual, gelu_pre, float(drop_p), _s64(seed))
 
 
+@_op("linear_dx_gelu", "(Tensor dy, Tensor w, Tensor pre, float drop_p, int seed) -> (Tensor, Tensor)")
+def _linear_dx_gelu(dy, w, pre, drop_p, seed):
+    return _K.linear_dx_gelu(dy, w, pre, drop_p, _u64(seed))
+
+
+@_linear_dx_gelu.register_fake
+def _(dy, w, pre, drop_p, seed):
+    return pre.new_empty(pre.shape), pre.new_empty(pre.shape)
+
+
+def linear_dx_gelu(dy, w, pre, drop_p=0.0, seed=0):
+    """fc2 dX through dropout(GELU(pre)) + h = dropout(GELU(pre)) as a side output."""
+    return torch.ops.ssl_mae.linear_dx_gelu(dy, w, pre, float(drop_p), _s64(seed))
+
+
 @_op("linear_dw", "(Tensor dy, Tensor x, Tensor(a!) grad_sink, bool accumulate) -> ()", ("grad_sink",))
 def _linear_dw(dy, x, grad_sink, accumulate):
     _K.linear_dw(dy, x, grad_sink, accumulate)
@@ -570,6 +585,29 @@ _conv3x3_fwd.register_fake(lambda x, w, F, H, W, Cin, Cout: x.new_empty((F * H *
 
 def conv3x3_fwd(x, wpack, F, H, W, Cin, Cout):
     return torch.ops.ssl_mae.conv3x3_fwd(x, wpack, F, H, W, Cin, Cout)
+
+
+@_op("conv3x3_fwd_bn_stats", "(Tensor x, Tensor wpack, int F, int H, int W, int Cin, int Cout, "
+                             "Tensor(a!)? running_mean, Tensor(b!)? running_var, float momentum, float eps, "
+                             "int updates, Tensor(c!)? num_batches_tracked) -> (Tensor, Tensor, Tensor)",
+     ("running_mean", "running_var", "num_batches_tracked"))
+def _conv3x3_fwd_bn_stats(x, wpack, F, H, W, Cin, Cout, running_mean, running_var, momentum, eps, updates,
+                          num_batches_tracked):
+    return _K.conv3x3_fwd_bn_stats(x, wpack, F, H, W, Cin, Cout, running_mean, running_var, momentum, eps, updates,
+                                   num_batches_tracked)
+
+
+@_conv3x3_fwd_bn_stats.register_fake
+def _(x, w, F, H, W, Cin, Cout, *a):
+    return (x.new_empty((F * H * W, Cout), dtype=torch.bfloat16), x.new_empty(Cout, dtype=torch.float32),
+            x.new_empty(Cout, dtype=torch.float32))
+
+
+def conv3x3_fwd_bn_stats(x, wpack, F, H, W, Cin, Cout, bn, updates=1):
+    """Stem conv2 + the train-mode statistics of its BatchNorm from the GEMM's epilogue."""
+    return torch.ops.ssl_mae.conv3x3_fwd_bn_stats(x, wpack, F, H, W, Cin, Cout, bn.running_mean, bn.running_var,
+                                                  float(bn.momentum), float(bn.eps), int(updates),
+                                                  bn.num_batches_tracked)
 
 
 @_op("conv3x3_dgrad", "(Tensor dy, Tensor wpack_t, int F, int H, int W, int Cin, int Cout) -> Tensor")

@@ -738,6 +738,24 @@ def test_linear_dw_bias_gelu_operand(M, N, H, p):
     assert rel_err(gw2, ref) < 2e-2
 
 
+@pytest.mark.parametrize("M,N,H,p", [(70000, 384, 1536, 0.1), (1001, 384, 1536, 0.0), (300, 96, 64, 0.1),
+                                     (6000, 192, 776, 0.1)])
+def test_linear_dx_gelu_side_output(M, N, H, p):
+    """fc2's data gradient through dropout(GELU(pre)) with h = dropout(GELU(pre)) as a side
+    output of the same epilogue (sm_linear_dx_gelu): dx bit-identical to linear_dx(gelu_pre)
+    and h bit-identical to the gelu kernel, at the decoder shape, without dropout, a
+    single-tile M and a ragged column tile (H = 776)."""
+    kk = KK()
+    pre = rnd(M, H, dtype=torch.bfloat16, seed=190).to(DEV)
+    dy = rnd(M, N, dtype=torch.bfloat16, seed=191, scale=0.1).to(DEV)
+    w = rnd(N, H, dtype=torch.bfloat16, seed=192, scale=0.05).to(DEV)
+    dx1 = kk.linear_dx(dy, w, gelu_pre=pre, drop_p=p, seed=77)
+    h1 = kk.gelu(pre, p, 77)
+    dx2, h2 = kk.linear_dx_gelu(dy, w, pre, p, 77)
+    assert torch.equal(dx1, dx2)
+    assert torch.equal(h1, h2)
+
+
 @pytest.mark.parametrize("Fr,HW,N,C,acc", [(3, 64, 96, 384, True), (5, 192, 96, 200, False), (2, 3136, 192, 768, True),
                                            (64, 12544, 96, 384, True), (1, 128, 8, 8, False)])
 def test_linear_dw_se_operand(Fr, HW, N, C, acc):
@@ -796,6 +814,29 @@ def test_linear_bn_stats(M, N, Kd, upd):
     yf = y1.float()
     assert rel_err(m2, yf.mean(0)) < 1e-4
     assert rel_err(r2, 1.0 / torch.sqrt(yf.var(0, unbiased=False) + 1e-5)) < 1e-4
+
+
+@pytest.mark.parametrize("Fn,H,W,Cin,Cout,upd", [(3, 14, 12, 48, 96, 1), (2, 9, 23, 16, 24, 2),
+                                                  (32, 112, 112, 48, 96, 1), (1, 3, 5, 8, 8, 1)])
+def test_conv3x3_fwd_bn_stats(Fn, H, W, Cin, Cout, upd):
+    """Stem conv2 + BN2 statistics from the implicit-conv GEMM's epilogue
+    (sm_conv3x3_fwd_bn_stats): y bit-identical to conv3x3_fwd, statistics / running
+    statistics within fp32 rounding of bn_stats over the same y.  Shapes: ragged pixel
+    tiles and 64-row slabs, the B = 8 clip frame count at 112^2 (32 frames), 15 pixels."""
+    kk = KK()
+    x = rnd(Fn * H * W, Cin, dtype=torch.bfloat16, seed=210).to(DEV)
+    wp = kk.conv_wpack(rnd(Cout, Cin, 3, 3, seed=211).to(DEV) * 0.1, 9 * Cin, 1, torch.bfloat16)
+    rm1, rv1 = torch.full((Cout,), 0.1, device=DEV), torch.full((Cout,), 2.0, device=DEV)
+    rm2, rv2 = rm1.clone(), rv1.clone()
+    nb1 = torch.zeros((), dtype=torch.int64, device=DEV)
+    nb2 = nb1.clone()
+    y1 = kk.conv3x3_fwd(x, wp, Fn, H, W, Cin, Cout)
+    m1, r1 = kk.bn_stats(y1, rm1, rv1, 0.1, 1e-5, upd, nb1)
+    y2, m2, r2 = kk.conv3x3_fwd_bn_stats(x, wp, Fn, H, W, Cin, Cout, rm2, rv2, 0.1, 1e-5, upd, nb2)
+    assert torch.equal(y1, y2)
+    assert rel_err(m2, m1) < 1e-5 and rel_err(r2, r1) < 1e-5
+    assert rel_err(rm2, rm1) < 1e-5 and rel_err(rv2, rv1) < 1e-5
+    assert int(nb2) == upd == int(nb1)
 
 
 @pytest.mark.parametrize("Fr,HW,N,C", [(3, 128, 96, 384), (2, 256, 192, 768), (16, 12544, 96, 384),
