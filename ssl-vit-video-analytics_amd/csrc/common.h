@@ -66,30 +66,56 @@ SM_DEV void store4(__bf16* p, const float* v) {
 // (Abramowitz & Stegun 7.1.26, |error| < 1.5e-7): Phi = erfc / 2 for x < 0 (no
 // cancellation in the left tail) and 1 - erfc / 2 for x >= 0.  The exp(-z^2) =
 // exp(-x^2 / 2) factor is shared with the normal pdf of the derivative, so GELU is one
-// rcp, one exp2 and a 5-term Horner chain, and its derivative adds two ops.  (The
-// previous Numerical-Recipes erfc needed a 10-term chain and a second exp2; these
-// functions sit in the VALU-bound BatchNorm / depthwise / SE / GEMM-epilogue loops.)
-// Every kernel uses these two functions, so recomputed activations are bit-identical
-// to stored ones.
-SM_DEV float gelu_phi_pair(float x, float* pdf_out) {
-  const float z = fabsf(x) * 0.70710678118654752f;
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
-  float p = 1.061405429f;
-  p = fmaf(p, t, -1.453152027f);
-  p = fmaf(p, t, 1.421413741f);
-  p = fmaf(p, t, -0.284496736f);
-  p = fmaf(p, t, 0.254829592f);
-  const float e = __builtin_amdgcn_exp2f(z * z * -1.44269504088896341f);
-  const float half_erfc = 0.5f * (p * t) * e;
-  if (pdf_out) *pdf_out = 0.39894228040143268f * e;
-  return x < 0.f ? half_erfc : 1.0f - half_erfc;
+// rcp, one exp2 and a 5-term Horner chain (its coefficients pre-halved: erfc / 2 directly),
+// and its derivative adds two ops.
+// One template for a scalar and a packed pair (f32x2: v_pk_fma_f32 / v_pk_mul_f32 /
+// v_pk_add_f32, two elements per VALU issue -- the f32 vector peak -- for the MFMA-free
+// streaming kernels): the same operation sequence with contraction off, so both forms,
+// and every kernel that evaluates GELU, produce bit-identical results (recomputed
+// activations equal stored ones).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+SM_DEV float vfma(float a, float b, float c) { return fmaf(a, b, c); }
+SM_DEV f32x2 vfma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+SM_DEV float vabs(float a) { return fabsf(a); }
+SM_DEV f32x2 vabs(f32x2 a) { return __builtin_elementwise_abs(a); }
+SM_DEV float vrcp(float a) { return __builtin_amdgcn_rcpf(a); }
+SM_DEV f32x2 vrcp(f32x2 a) { return f32x2{__builtin_amdgcn_rcpf(a.x), __builtin_amdgcn_rcpf(a.y)}; }
+SM_DEV float vexp2(float a) { return __builtin_amdgcn_exp2f(a); }
+SM_DEV f32x2 vexp2(f32x2 a) { return f32x2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)}; }
+SM_DEV float vsel_neg(float x, float a, float b) { return x < 0.f ? a : b; }   // x < 0 ? a : b
+SM_DEV f32x2 vsel_neg(f32x2 x, f32x2 a, f32x2 b) { return f32x2{x.x < 0.f ? a.x : b.x, x.y < 0.f ? a.y : b.y}; }
+
+template <typename V>
+SM_DEV V gelu_phi_pair_t(V x, V* pdf_out) {
+#pragma clang fp contract(off)
+  const V t = vrcp(vfma(vabs(x), V(0.3275911f * 0.70710678118654752f), V(1.0f)));
+  V p = V(0.5f * 1.061405429f);
+  p = vfma(p, t, V(0.5f * -1.453152027f));
+  p = vfma(p, t, V(0.5f * 1.421413741f));
+  p = vfma(p, t, V(0.5f * -0.284496736f));
+  p = vfma(p, t, V(0.5f * 0.254829592f));
+  const V e = vexp2((x * x) * V(-0.5f * 1.44269504088896341f));
+  const V half_erfc = (p * t) * e;
+  if (pdf_out) *pdf_out = e * V(0.39894228040143268f);
+  return vsel_neg(x, half_erfc, V(1.0f) - half_erfc);
 }
-SM_DEV float gelu_f(float x) { return x * gelu_phi_pair(x, nullptr); }
-SM_DEV float gelu_grad(float x) {
-  float pdf;
-  const float cdf = gelu_phi_pair(x, &pdf);
-  return cdf + x * pdf;
+template <typename V>
+SM_DEV V gelu_t(V x) {
+#pragma clang fp contract(off)
+  return x * gelu_phi_pair_t<V>(x, nullptr);
 }
+template <typename V>
+SM_DEV V gelu_grad_t(V x) {
+#pragma clang fp contract(off)
+  V pdf;
+  const V cdf = gelu_phi_pair_t<V>(x, &pdf);
+  return vfma(x, pdf, cdf);
+}
+SM_DEV float gelu_phi_pair(float x, float* pdf_out) { return gelu_phi_pair_t<float>(x, pdf_out); }
+SM_DEV float gelu_f(float x) { return gelu_t<float>(x); }
+SM_DEV float gelu_grad(float x) { return gelu_grad_t<float>(x); }
+SM_DEV f32x2 gelu_f2(f32x2 x) { return gelu_t<f32x2>(x); }
+SM_DEV f32x2 gelu_grad2(f32x2 x) { return gelu_grad_t<f32x2>(x); }
 
 // Per-channel input transform folded into a consumer's loads: h = act(x * sc + sh)
 // with sc = rstd * w, sh = b - mean * sc (train-mode BatchNorm) and act = GELU or
@@ -117,13 +143,16 @@ struct Affine8 {
     }
   }
   // v: 8 values loaded from T storage -> the stored-precision activation
+  // (packed pairs: see gelu_phi_pair_t)
   template <typename T>
   SM_DEV void apply(float* v) const {
     if (!on) return;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float t = v[j] * sc[j] + sh[j];
-      v[j] = to_f<T>(from_f<T>(gelu ? gelu_f(t) : t));
+    for (int j = 0; j < 8; j += 2) {
+      f32x2 t = vfma(f32x2{v[j], v[j + 1]}, f32x2{sc[j], sc[j + 1]}, f32x2{sh[j], sh[j + 1]});
+      if (gelu) t = gelu_f2(t);
+      v[j] = to_f<T>(from_f<T>(t.x));
+      v[j + 1] = to_f<T>(from_f<T>(t.y));
     }
   }
 };

@@ -668,13 +668,22 @@ __global__ __launch_bounds__(256, 2) void dwb_kernel(const __bf16* dy, const __b
         for (int p = 0; p < PX; ++p) {
           const bool ok = xi0 + p < W;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float u = fmaf((float)xs[p][j], sc[j], sh[j]);
-            float cdf = 1.f, pdf = 0.f;
-            if (GELU) cdf = gelu_phi_pair(u, &pdf);
-            h[p][j] = ok ? (float)(__bf16)(GELU ? u * cdf : u) : 0.f;
-            gg[p][j] = ok ? fmaf(u, pdf, cdf) : 0.f;
-            g[p][j] = 0.f;
+          for (int j = 0; j < 4; j += 2) {   // packed pairs (gelu_phi_pair_t)
+            const f32x2 u = vfma(f32x2{(float)xs[p][j], (float)xs[p][j + 1]}, f32x2{sc[j], sc[j + 1]},
+                                 f32x2{sh[j], sh[j + 1]});
+            f32x2 cdf = f32x2{1.f, 1.f}, pdf = f32x2{0.f, 0.f};
+            if (GELU) cdf = gelu_phi_pair_t<f32x2>(u, &pdf);
+            f32x2 hv = u;
+            if (GELU) {
+#pragma clang fp contract(off)
+              hv = u * cdf;
+            }
+            const f32x2 gv = vfma(u, pdf, cdf);
+            h[p][j] = ok ? (float)(__bf16)hv.x : 0.f;
+            h[p][j + 1] = ok ? (float)(__bf16)hv.y : 0.f;
+            gg[p][j] = ok ? gv.x : 0.f;
+            gg[p][j + 1] = ok ? gv.y : 0.f;
+            g[p][j] = g[p][j + 1] = 0.f;
           }
           __builtin_amdgcn_sched_barrier(0);   // bound the interleaved GELU chains (VGPR budget)
         }
@@ -831,13 +840,22 @@ __global__ __launch_bounds__(256, 2) void dwb2_kernel(const __bf16* dy, const __
         for (int p = 0; p < PX; ++p) {
           const bool ok = xi0 + p < W;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float u = fmaf((float)xs[p][j], sc[j], sh[j]);
-            float cdf = 1.f, pdf = 0.f;
-            if (GELU) cdf = gelu_phi_pair(u, &pdf);
-            h[p][j] = ok ? (float)(__bf16)(GELU ? u * cdf : u) : 0.f;
-            gg[p][j] = ok ? fmaf(u, pdf, cdf) : 0.f;
-            g[p][j] = 0.f;
+          for (int j = 0; j < 4; j += 2) {   // packed pairs (gelu_phi_pair_t)
+            const f32x2 u = vfma(f32x2{(float)xs[p][j], (float)xs[p][j + 1]}, f32x2{sc[j], sc[j + 1]},
+                                 f32x2{sh[j], sh[j + 1]});
+            f32x2 cdf = f32x2{1.f, 1.f}, pdf = f32x2{0.f, 0.f};
+            if (GELU) cdf = gelu_phi_pair_t<f32x2>(u, &pdf);
+            f32x2 hv = u;
+            if (GELU) {
+#pragma clang fp contract(off)
+              hv = u * cdf;
+            }
+            const f32x2 gv = vfma(u, pdf, cdf);
+            h[p][j] = ok ? (float)(__bf16)hv.x : 0.f;
+            h[p][j + 1] = ok ? (float)(__bf16)hv.y : 0.f;
+            gg[p][j] = ok ? gv.x : 0.f;
+            gg[p][j + 1] = ok ? gv.y : 0.f;
+            g[p][j] = g[p][j + 1] = 0.f;
           }
           __builtin_amdgcn_sched_barrier(0);   // bound the interleaved GELU chains (VGPR budget)
         }
@@ -1208,20 +1226,30 @@ __global__ __launch_bounds__(256) void se_bn_reduce_kernel(const T* dy, const T*
       load8(x + e, v);
       load8(dy + e, g);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float xh = fmaf(v[j], bc.rs[j], -bc.mr[j]);
-        const float u = fmaf(v[j], bc.sc[j], bc.sh[j]);
-        float pdf;
-        const float cdf = gelu_phi_pair(u, &pdf);
-        const float h = to_f<T>(from_f<T>(u * cdf));   // the stored-precision SE input
-        const float gp = act.gelu ? fmaf(u, pdf, cdf) : 1.f;
-        const float hh = act.gelu ? h : to_f<T>(from_f<T>(u));
-        const float t = gp * xh;
-        acc[0][j] = fmaf(g[j], hh, acc[0][j]);
-        acc[1][j] = fmaf(g[j], gp, acc[1][j]);
-        acc[2][j] += gp;
-        acc[3][j] = fmaf(g[j], t, acc[3][j]);
-        acc[4][j] += t;
+      for (int j = 0; j < 8; j += 2) {   // packed pairs (gelu_phi_pair_t)
+        const f32x2 vv = f32x2{v[j], v[j + 1]};
+        const f32x2 u = vfma(vv, f32x2{bc.sc[j], bc.sc[j + 1]}, f32x2{bc.sh[j], bc.sh[j + 1]});
+        f32x2 pdf;
+        const f32x2 cdf = gelu_phi_pair_t<f32x2>(u, &pdf);
+        f32x2 hv;
+        {
+#pragma clang fp contract(off)
+          hv = u * cdf;
+        }
+        const f32x2 gv = vfma(u, pdf, cdf);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const float xh = fmaf(v[j + i], bc.rs[j + i], -bc.mr[j + i]);
+          const float h = to_f<T>(from_f<T>(hv[i]));   // the stored-precision SE input
+          const float gp = act.gelu ? gv[i] : 1.f;
+          const float hh = act.gelu ? h : to_f<T>(from_f<T>(u[i]));
+          const float t = gp * xh;
+          acc[0][j + i] = fmaf(g[j + i], hh, acc[0][j + i]);
+          acc[1][j + i] = fmaf(g[j + i], gp, acc[1][j + i]);
+          acc[2][j + i] += gp;
+          acc[3][j + i] = fmaf(g[j + i], t, acc[3][j + i]);
+          acc[4][j + i] += t;
+        }
       }
     }
   }
@@ -1295,11 +1323,17 @@ __global__ __launch_bounds__(256) void se_bn_dx_kernel(const T* dy, const T* x, 
     load8(x + e, v);
     load8(dy + e, g);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float xh = fmaf(v[j], bc.rs[j], -bc.mr[j]);
-      float du = fmaf(g[j], ss[j], ad[j]);
-      if (act.gelu) du *= gelu_grad(fmaf(v[j], bc.sc[j], bc.sh[j]));
-      o[j] = bc.wr[j] * (du - k0[j] - xh * k1[j]);
+    for (int j = 0; j < 8; j += 2) {   // packed pairs (gelu_phi_pair_t)
+      f32x2 gd = f32x2{1.f, 1.f};
+      if (act.gelu)
+        gd = gelu_grad2(vfma(f32x2{v[j], v[j + 1]}, f32x2{bc.sc[j], bc.sc[j + 1]}, f32x2{bc.sh[j], bc.sh[j + 1]}));
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const float xh = fmaf(v[j + i], bc.rs[j + i], -bc.mr[j + i]);
+        float du = fmaf(g[j + i], ss[j + i], ad[j + i]);
+        if (act.gelu) du *= gd[i];
+        o[j + i] = bc.wr[j + i] * (du - k0[j + i] - xh * k1[j + i]);
+      }
     }
     store8(dx + e, o);
   }

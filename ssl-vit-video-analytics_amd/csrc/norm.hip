@@ -422,9 +422,11 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const TI* x, const float*
     float v[8];
     load8(x + e, v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float t = v[j] * sc[j] + sh[j];
-      v[j] = gelu ? gelu_f(t) : t;
+    for (int j = 0; j < 8; j += 2) {   // packed pairs (gelu_phi_pair_t); = Affine8::apply
+      f32x2 t = vfma(f32x2{v[j], v[j + 1]}, f32x2{sc[j], sc[j + 1]}, f32x2{sh[j], sh[j + 1]});
+      if (gelu) t = gelu_f2(t);
+      v[j] = t.x;
+      v[j + 1] = t.y;
     }
     if (row_scale) {
       const float rs = row_scale[row / rpg];
@@ -466,12 +468,15 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const TD* dy, const 
       load4(dy + row * ld + cm.chunk * 4, dv);
       const float rsc = row_scale ? row_scale[row / rpg] : 1.f;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float xh = (xv[j] - mu[j]) * rs[j];
-        float gg = dv[j] * rsc;
-        if (gelu) gg *= gelu_grad(xh * ww[j] + bb[j]);
-        sg[j] += gg;
-        sgx[j] += gg * xh;
+      for (int j = 0; j < 4; j += 2) {   // packed pairs (gelu_phi_pair_t)
+        const f32x2 xh = (f32x2{xv[j], xv[j + 1]} - f32x2{mu[j], mu[j + 1]}) * f32x2{rs[j], rs[j + 1]};
+        f32x2 gg = f32x2{dv[j], dv[j + 1]} * rsc;
+        if (gelu) gg *= gelu_grad2(vfma(xh, f32x2{ww[j], ww[j + 1]}, f32x2{bb[j], bb[j + 1]}));
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          sg[j + i] += gg[i];
+          sgx[j + i] += gg[i] * xh[i];
+        }
       }
     }
   }
@@ -527,11 +532,12 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const TD* dy, const TI* 
     load8(dy + e, dv);
     const float rsc = row_scale ? row_scale[row / rpg] : 1.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float xh = (xv[j] - mu[j]) * rs[j];
-      float gg = dv[j] * rsc;
-      if (gelu) gg *= gelu_grad(xh * ww[j] + bb[j]);
-      o[j] = ww[j] * rs[j] * (gg - k0[j] - xh * k1[j]);
+    for (int j = 0; j < 8; j += 2) {   // packed pairs (gelu_phi_pair_t)
+      const f32x2 xh = (f32x2{xv[j], xv[j + 1]} - f32x2{mu[j], mu[j + 1]}) * f32x2{rs[j], rs[j + 1]};
+      f32x2 gg = f32x2{dv[j], dv[j + 1]} * rsc;
+      if (gelu) gg *= gelu_grad2(vfma(xh, f32x2{ww[j], ww[j + 1]}, f32x2{bb[j], bb[j + 1]}));
+#pragma unroll
+      for (int i = 0; i < 2; ++i) o[j + i] = ww[j + i] * rs[j + i] * (gg[i] - k0[j + i] - xh[i] * k1[j + i]);
     }
     store8(dx + e, o);
   }
@@ -562,7 +568,11 @@ __global__ void gelu_bwd_kernel(const T* pre, const TG* dy, TG* dx, int64_t tota
     load8(dy + i * 8, d);
     if (drop_p > 0.f) drop_mult8(i * 8, ncols, drop_p, seed, m);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) d[j] *= (drop_p > 0.f ? m[j] : 1.f) * gelu_grad(p[j]);
+    for (int j = 0; j < 8; j += 2) {
+      const f32x2 gd = gelu_grad2(f32x2{p[j], p[j + 1]});
+      d[j] *= (drop_p > 0.f ? m[j] : 1.f) * gd.x;
+      d[j + 1] *= (drop_p > 0.f ? m[j + 1] : 1.f) * gd.y;
+    }
     store8(dx + i * 8, d);
   }
 }
@@ -626,7 +636,11 @@ __global__ void gelu_fwd_kernel(const T* x, T* y, int64_t total8, int ncols, flo
     load8(x + i * 8, v);
     if (drop_p > 0.f) drop_mult8(i * 8, ncols, drop_p, seed, m);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = gelu_f(v[j]) * (drop_p > 0.f ? m[j] : 1.f);
+    for (int j = 0; j < 8; j += 2) {
+      const f32x2 gv = gelu_f2(f32x2{v[j], v[j + 1]});
+      v[j] = gv.x * (drop_p > 0.f ? m[j] : 1.f);
+      v[j + 1] = gv.y * (drop_p > 0.f ? m[j + 1] : 1.f);
+    }
     store8(y + i * 8, v);
   }
 }
