@@ -178,6 +178,27 @@ int sm_conv_wpack(int out_dtype, const float* src, void* dst, int Cout, int Cin,
                   hipStream_t st);
 int sm_conv_wunpack_add(const float* packed, float* grad, int Cout, int Cin, int Kpad, int order,
                         hipStream_t st);
+/* Stem conv1 (tiny_vit.py:67: 3 -> 48, 3x3, stride 2, pad 1) straight from the fp32 clip
+ * (strides as sm_stem_im2col) on the matrix cores, plus the train-mode BatchNorm statistics
+ * of its bf16 output y [B*T*Ho*Wo][48] (tiny_vit.py:68, as sm_linear_bn_stats): replaces
+ * sm_stem_im2col + sm_linear_bn_stats (y bit-identical), no [pixels][32] buffer.
+ * wpack = sm_conv_wpack order 0 [48][32] bf16. */
+int64_t sm_stem_conv1_workspace_bytes(void);
+int sm_stem_conv1_bn_stats(const float* clip, int B, int T, int H, int W, int64_t sB, int64_t sC, int64_t sT,
+                           int64_t sH, int64_t sW, const void* wpack, void* y, float* mean, float* rstd,
+                           float* run_mean, float* run_var, int64_t* num_batches_tracked, float momentum, float eps,
+                           int updates, void* ws, int64_t ws_bytes, hipStream_t st);
+/* Stem conv2 over h1 = act(BN1(a1)) (tiny_vit.py:68-70: BN1 + GELU, 3x3 48 -> 96 stride 1
+ * pad 1) plus the train-mode BatchNorm statistics of its bf16 output, one frame per
+ * workgroup: BN1 + GELU applied once per element into an LDS ring of h1 rows, so h1 is
+ * never written (y bit-identical to sm_bn_apply + sm_conv3x3_fwd).  a1 [F*H*W][48] bf16,
+ * wpack = sm_conv_wpack order 1 [96][432] bf16, y [F*H*W][96] bf16, W <= 128; BN1 =
+ * (mean, rstd, weight, bias), gelu = act is GELU.  Workspace sm_stem_conv2_workspace_bytes(F). */
+int64_t sm_stem_conv2_workspace_bytes(int F);
+int sm_stem_conv2_bn_stats(const void* a1, int F, int H, int W, const float* bn1_mean, const float* bn1_rstd,
+                           const float* bn1_w, const float* bn1_b, int gelu, const void* wpack, void* y, float* mean,
+                           float* rstd, float* run_mean, float* run_var, int64_t* num_batches_tracked, float momentum,
+                           float eps, int updates, void* ws, int64_t ws_bytes, hipStream_t st);
 /* Stem conv2 (tiny_vit.py:69, 3x3 / stride 1 / pad 1, bf16, channels-last) as GEMMs over
  * the implicit im2col matrix -- no [pixels][9C] buffer in HBM.  wpack = sm_conv_wpack
  * order 1 ([Cout][9*Cin]); wpack_t = order 2 ([Cin][9*Cout]); Cin, Cout % 8 == 0.

@@ -172,6 +172,33 @@ def gemmk(args):
         torch.cuda.empty_cache()
 
 
+def stem(args):
+    """PatchEmbed forward pieces at B clips of 8x224^2 (bf16), HIP-event timed."""
+    dev = "cuda"
+    clip = torch.randn(args.batch, 3, 8, 224, 224, device=dev)
+    w1p = K.conv_wpack(torch.randn(48, 3, 3, 3, device=dev) * 0.2, 32, 0, torch.bfloat16)
+    w2p = K.conv_wpack(torch.randn(96, 48, 3, 3, device=dev) * 0.05, 432, 1, torch.bfloat16)
+    g1, b1 = torch.rand(48, device=dev) + 0.5, torch.randn(48, device=dev) * 0.1
+    g2, b2 = torch.rand(96, device=dev) + 0.5, torch.randn(96, device=dev) * 0.1
+    Fr, Ho, Wo = args.batch * 8, 112, 112
+
+    def rep(name, ms):
+        print(f"{name:34s} {ms:8.3f} ms", flush=True)
+    rep("stem_im2col", timeit(lambda: K.stem_im2col(clip, torch.bfloat16), args.iters))
+    col, _ = K.stem_im2col(clip, torch.bfloat16)
+    rep("conv1 GEMM + BN1 stats (im2col in)", timeit(lambda: K.linear_bn_stats(col, w1p), args.iters))
+    del col
+    rep("stem_conv1_bn_stats (direct)", timeit(lambda: K.stem_conv1_bn_stats(clip, w1p), args.iters))
+    a1, m1, r1, _ = K.stem_conv1_bn_stats(clip, w1p)
+    rep("stem_conv2_bn_stats (direct, act in ring)",
+        timeit(lambda: K.stem_conv2_bn_stats(a1, (m1, r1, g1, b1, True), w2p, Fr, Ho, Wo), args.iters))
+    rep("bn_apply + GELU (h1)", timeit(lambda: K.bn_apply(a1, m1, r1, g1, b1, gelu=True), args.iters))
+    h1 = K.bn_apply(a1, m1, r1, g1, b1, gelu=True)
+    rep("conv3x3_fwd_bn_stats", timeit(lambda: K.conv3x3_fwd_bn_stats(h1, w2p, Fr, Ho, Wo, 48, 96), args.iters))
+    a2, m2, r2 = K.conv3x3_fwd_bn_stats(h1, w2p, Fr, Ho, Wo, 48, 96)
+    rep("bn_apply (y)", timeit(lambda: K.bn_apply(a2, m2, r2, g2, b2, gelu=False), args.iters))
+
+
 def mbconv(args):
     """Stage-0 MBConv streaming ops at F = batch*8 frames of 112x112x384 (bf16)."""
     Fn, H, W, C = args.batch * 8, 112, 112, 384
@@ -226,7 +253,7 @@ def mbconv(args):
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["attn", "gemm", "gemmk", "mbconv", "dw", "dwx", "dwse"])
+    ap.add_argument("what", choices=["attn", "gemm", "gemmk", "mbconv", "dw", "dwx", "dwse", "stem"])
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--drop", type=float, default=0.1)
     ap.add_argument("--iters", type=int, default=5)
@@ -234,4 +261,4 @@ if __name__ == "__main__":
     a = ap.parse_args()
     from ssl_mae_amd.build import build
     build()
-    {"attn": attn, "gemm": gemm, "gemmk": gemmk, "mbconv": mbconv, "dw": dw, "dwx": dwx, "dwse": dwse}[a.what](a)
+    {"attn": attn, "gemm": gemm, "gemmk": gemmk, "mbconv": mbconv, "dw": dw, "dwx": dwx, "dwse": dwse, "stem": stem}[a.what](a)

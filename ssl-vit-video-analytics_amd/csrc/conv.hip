@@ -10,6 +10,8 @@
 //  * depthwise 3x3 conv (MBConv, tiny_vit.py:46) fwd, dgrad, wgrad; 8 channels/thread.
 //  * SE layer (tiny_vit.py:20-34): per-frame channel mean, the two tiny FCs fused
 //    per frame, and the broadcast scale, each with its backward.
+#include <algorithm>
+
 #include "common.h"
 #include "sm_api.h"
 
@@ -55,6 +57,277 @@ __global__ void stem_im2col_kernel(ClipView v, int Ho, int Wo, int stride, TO* c
     TO* o = col + i * 32;
 #pragma unroll
     for (int k = 0; k < 32; k += 8) store8(o + k, vals + k);
+  }
+}
+
+// ------------------------------------------------------------------ stem conv1, direct
+// PatchEmbed conv1 (tiny_vit.py:67: 3 -> 48, 3x3, stride 2, pad 1) straight from the fp32
+// clip, no im2col buffer: a wave takes 32 consecutive output pixels, each lane gathers its
+// pixel's 16 of the 32 (ci, ky, kx) inputs (K order of stem_im2col, 27 -> 32) as bf16
+// A-operand fragments of two v_mfma_f32_32x32x16_bf16 steps per 32-channel block (the
+// same products and order as the im2col GEMM's single K-step: bit-identical a1).  Output
+// lane = channel, registers = 16 pixels: the BatchNorm-1 sums of the stored bf16 values
+// are two registers per lane and block; the bf16 tile goes through a per-wave LDS image
+// [32 px][48 ch] to 16-B row stores.  One fixed-order reduction per block ->
+// part[block][2][48].  Tap offsets are wave-uniform (scalar) per lane half.
+constexpr int SC1_BLOCKS = 2048, SC1_COUT = 48, SC1_PITCH = 56;   // image row: 48 ch + 8 pad (bf16)
+
+__global__ __launch_bounds__(256, 4) void stem_conv1_kernel(ClipView v, int Ho, int Wo, const __bf16* w /*[48][32]*/,
+                                                         __bf16* y /*[P][48]*/, float* part /*[grid][2][48]*/) {
+  __shared__ __attribute__((aligned(16))) __bf16 img[4][32 * SC1_PITCH];
+  __shared__ float red[4][2][64];
+  const int l = threadIdx.x & 63, h = l >> 5, wv = threadIdx.x >> 6;
+  const int P = v.B * v.T * Ho * Wo;   // host: < 2^31
+  const int nseg = (P + 31) / 32;
+  bf16x8 wf[2][2];   // B fragments: co = 32 j + (l & 31), k = 16 s + 8 h + 0..7
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int co = 32 * j + (l & 31);
+      if (co < SC1_COUT) wf[j][s] = *(const bf16x8*)(w + co * 32 + 16 * s + 8 * h);
+      else
+#pragma unroll
+        for (int e = 0; e < 8; ++e) wf[j][s][e] = (__bf16)0.f;
+    }
+  float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};   // channel 32 j + (l & 31), this lane's pixels
+  const int HWo = Ho * Wo;
+  __bf16* im = img[wv];
+  for (int seg = blockIdx.x * 4 + wv; seg < nseg; seg += gridDim.x * 4) {
+    const int px = seg * 32 + (l & 31);
+    const bool ok = px < P;
+    const int f = px / HWo, rem = px - f * HWo;
+    const int yo = rem / Wo, xo = rem - yo * Wo;
+    const float* base = v.p + (int64_t)(f / v.T) * v.sB + (int64_t)(f % v.T) * v.sT + (2 * yo) * v.sH + (2 * xo) * v.sW;
+    bf16x8 af[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        // k = 16 s + 8 h + e: both halves' taps are compile-time, the offsets scalar
+        const int k0 = 16 * s + e, k1 = k0 + 8;
+        const int ky = h ? (k1 % 9) / 3 : (k0 % 9) / 3, kx = h ? k1 % 3 : k0 % 3;
+        const bool kin = h ? k1 < 27 : k0 < 27;
+        const int off = h ? (int)((k1 / 9) * v.sC + ((k1 % 9) / 3 - 1) * v.sH + (k1 % 3 - 1) * v.sW)
+                          : (int)((k0 / 9) * v.sC + ((k0 % 9) / 3 - 1) * v.sH + (k0 % 3 - 1) * v.sW);
+        const int yi = 2 * yo + ky - 1, xi = 2 * xo + kx - 1;
+        // unconditional loads (padding reads the clip's first element, then zero): the
+        // sixteen gathers issue back to back instead of one branch each
+        const bool in = ok && kin && (unsigned)yi < (unsigned)v.H && (unsigned)xi < (unsigned)v.W;
+        const float x = *(in ? base + off : v.p);
+        af[s][e] = (__bf16)(in ? x : 0.f);
+      }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], wf[j][s], acc, 0, 0, 0);
+      const int co = 32 * j + (l & 31);
+      if (co < SC1_COUT) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {   // pixel (r & 3) + 8 (r >> 2) + 4 h of the segment
+          const int pp = (r & 3) + 8 * (r >> 2) + 4 * h;
+          const __bf16 o = (__bf16)acc[r];
+          if (seg * 32 + pp < P) {
+            const float of = (float)o;
+            s1[j] += of;
+            s2[j] = fmaf(of, of, s2[j]);
+          }
+          im[pp * SC1_PITCH + co] = o;
+        }
+      }
+    }
+    // the wave's [32 px][48 ch] image -> 16-B runs (6 per pixel, 3 per lane)
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int c = l + 64 * i, pp = c / 6, ch = c - pp * 6;
+      const uint4 val = *(const uint4*)(im + pp * SC1_PITCH + ch * 8);
+      if (seg * 32 + pp < P) *(uint4*)(y + (int64_t)(seg * 32 + pp) * SC1_COUT + ch * 8) = val;
+    }
+  }
+  // fixed-order reduction: the two halves of each wave (the same channels), then the 4 waves
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    s1[j] += __shfl_xor(s1[j], 32, 64);
+    s2[j] += __shfl_xor(s2[j], 32, 64);
+  }
+  if (h == 0) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      red[wv][0][32 * j + l] = s1[j];
+      red[wv][1][32 * j + l] = s2[j];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * SC1_COUT) {
+    const int which = threadIdx.x / SC1_COUT, co = threadIdx.x % SC1_COUT;
+    part[((int64_t)blockIdx.x * 2 + which) * SC1_COUT + co] =
+        ((red[0][which][co] + red[1][which][co]) + red[2][which][co]) + red[3][which][co];
+  }
+}
+
+// ------------------------------------------------------------------ stem conv2, direct
+// PatchEmbed conv2 (tiny_vit.py:69: 48 -> 96, 3x3, stride 1, pad 1) over h1 =
+// GELU(BN1(a1)) (tiny_vit.py:68) with BN2's statistics (tiny_vit.py:70): block = one
+// frame, walked in bands of SC2_R output rows.  BN1 + GELU is applied ONCE per input
+// element while a row enters an LDS ring of h1 rows (zero halo = the conv's padding of
+// h1), so neither h1 nor a 9x im2col exists in HBM.  12 waves = 3 channel blocks x 4
+// pixel segments of 32.  The packed weights [96][432] stay in LDS for the block; per
+// band and tap row each wave loads its 32 channels' 9 B fragments into registers and
+// reads the pixel A fragments from the ring (ds_read_b128; 112-B pixel and 880-B
+// weight-row pitches: conflict-free).  K order (tap, ci) and the 16-wide k-steps are the
+// implicit-im2col GEMM's, so y is bit-identical to conv3x3_fwd(bn_apply(a1)).  Output
+// lane = channel: BN2 sums in 2 registers; each store instruction writes 64-B channel
+// runs of two pixels.
+constexpr int SC2_CIN = 48, SC2_COUT = 96, SC2_K = 432, SC2_R = 2, SC2_NR = SC2_R + 2;
+constexpr int SC2_PXS = 130, SC2_PITCH = 56, SC2_WPITCH = 440;   // bf16 units
+constexpr int SC2_NW = 12, SC2_NT = SC2_NW * 64, SC2_CHUNKS = 2;  // staged 16-B chunks per thread per band
+constexpr int SC2_RING = SC2_NR * SC2_PXS * SC2_PITCH * 2, SC2_LDS = SC2_RING + SC2_COUT * SC2_WPITCH * 2;
+
+template <bool GELU>
+__global__ __launch_bounds__(SC2_NT, 1) void stem_conv2_kernel(const __bf16* a1, ChanAffine act,
+                                                               const __bf16* wpack /*[96][432]*/, __bf16* y,
+                                                               float* part /*[F][2][96]*/, int H, int W) {
+  __shared__ __attribute__((aligned(16))) char lds[SC2_LDS];   // static: > 64 KB (gfx950: 160 KB per CU)
+  __shared__ float aff[2][SC2_CIN];
+  __shared__ float red[SC2_NW][2][32];
+  __bf16* ring = (__bf16*)lds;
+  __bf16* wl = (__bf16*)(lds + SC2_RING);
+  const int t = threadIdx.x, l = t & 63, h = l >> 5, wv = t >> 6;
+  const int nb = wv % 3, sg = wv / 3;
+  const int64_t f = blockIdx.x;
+  const __bf16* src = a1 + f * H * W * SC2_CIN;
+  if (t < SC2_CIN) {   // = Affine8::init
+    const float sc = act.rstd[t] * act.w[t];
+    aff[0][t] = sc;
+    aff[1][t] = act.b[t] - act.mean[t] * sc;
+  }
+  // zero the ring once: halo columns (x = -1, x >= W) and rows outside the image
+  for (int i = t; i < SC2_RING / 16; i += SC2_NT) *(uint4*)(lds + 16 * i) = make_uint4(0, 0, 0, 0);
+  for (int i = t; i < SC2_COUT * SC2_K / 8; i += SC2_NT) {
+    const int co = i / (SC2_K / 8), k8 = i - co * (SC2_K / 8);
+    *(uint4*)(wl + co * SC2_WPITCH + 8 * k8) = *(const uint4*)(wpack + co * SC2_K + 8 * k8);
+  }
+  // this thread's chunks of a band's rows: (row, pixel, 8-channel group) packed
+  const int rowc = W * (SC2_CIN / 8);
+  int cpos[SC2_CHUNKS];
+#pragma unroll
+  for (int i = 0; i < SC2_CHUNKS; ++i) {
+    const int c = t + SC2_NT * i;
+    const int r = c / rowc, rem = c - r * rowc, x = rem / 6;
+    cpos[i] = r < SC2_R ? (r << 16) | (x << 3) | (rem - x * 6) : -1;
+  }
+  __syncthreads();
+  auto slot = [&](int iy) { return (iy + 1) % SC2_NR; };
+  uint4 raw[SC2_CHUNKS];
+  auto load_rows = [&](int iy0) {   // rows iy0 .. iy0 + SC2_R - 1 of a1 (past H: zero)
+#pragma unroll
+    for (int i = 0; i < SC2_CHUNKS; ++i) {
+      const int iy = iy0 + (cpos[i] >> 16);
+      raw[i] = make_uint4(0, 0, 0, 0);
+      if (cpos[i] >= 0 && iy < H)
+        raw[i] = *(const uint4*)(src + ((int64_t)iy * W + ((cpos[i] >> 3) & 0x1FFF)) * SC2_CIN + 8 * (cpos[i] & 7));
+    }
+  };
+  // BN1 + GELU (packed pairs, = bn_apply) of chunk i into its ring row; rows past H are
+  // the conv's zero padding of h1
+  auto commit_chunk = [&](int i, int iy) {
+    const int x = (cpos[i] >> 3) & 0x1FFF, cc = cpos[i] & 7;
+    float vv[8];
+    load8((const __bf16*)&raw[i], vv);
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      f32x2 u = vfma(f32x2{vv[j], vv[j + 1]}, f32x2{aff[0][8 * cc + j], aff[0][8 * cc + j + 1]},
+                     f32x2{aff[1][8 * cc + j], aff[1][8 * cc + j + 1]});
+      if (GELU) u = gelu_f2(u);
+      vv[j] = iy < H ? u.x : 0.f;
+      vv[j + 1] = iy < H ? u.y : 0.f;
+    }
+    store8(ring + (slot(iy) * SC2_PXS + x + 1) * SC2_PITCH + 8 * cc, vv);
+  };
+  auto commit_rows = [&](int iy0) {
+#pragma unroll
+    for (int i = 0; i < SC2_CHUNKS; ++i)
+      if (cpos[i] >= 0) commit_chunk(i, iy0 + (cpos[i] >> 16));
+  };
+  // first band: input rows 0 .. SC2_R (row -1 stays zero)
+  load_rows(0);
+  commit_rows(0);
+  load_rows(SC2_R);   // only its first row (SC2_R) belongs to band 0
+#pragma unroll
+  for (int i = 0; i < SC2_CHUNKS; ++i)
+    if (cpos[i] >= 0 && (cpos[i] >> 16) == 0) commit_chunk(i, SC2_R);
+  float s1 = 0.f, s2 = 0.f;   // BN2 sums of channel 32 nb + (l & 31) over this lane's pixels
+  const int nbands = (H + SC2_R - 1) / SC2_R;
+  const int co = 32 * nb + (l & 31);
+  const __bf16* wrow = wl + co * SC2_WPITCH + 8 * h;
+  for (int band = 0; band < nbands; ++band) {
+    const int y0 = band * SC2_R;
+    if (band > 0) {
+      __syncthreads();   // the previous band finished reading the slots rewritten here
+      commit_rows(y0 + 1);   // rows y0 + 1, y0 + 2 (loaded during the previous band)
+    }
+    __syncthreads();
+    if (band + 1 < nbands) load_rows(y0 + SC2_R + 1);   // the next band's new rows, in flight
+    // both rows of the band accumulate tap row by tap row (k order (tap, ci) as the GEMM);
+    // per tap row ky the wave holds its 9 B fragments (k = 48 (3 ky + kx) + 16 c16 + 8 h)
+    f32x16 acc[SC2_R];
+#pragma unroll
+    for (int yy = 0; yy < SC2_R; ++yy)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[yy][r] = 0.f;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      bf16x8 wf[9];
+#pragma unroll
+      for (int q = 0; q < 9; ++q) wf[q] = *(const bf16x8*)(wrow + 16 * (9 * ky + q));
+#pragma unroll
+      for (int yy = 0; yy < SC2_R; ++yy) {
+        const __bf16* rp = ring + (slot(y0 + yy + ky - 1) * SC2_PXS + sg * 32 + (l & 31)) * SC2_PITCH + 8 * h;
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+          for (int c16 = 0; c16 < 3; ++c16)
+            acc[yy] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*(const bf16x8*)(rp + kx * SC2_PITCH + 16 * c16),
+                                                              wf[3 * kx + c16], acc[yy], 0, 0, 0);
+        if (yy + 1 < SC2_R) __builtin_amdgcn_sched_barrier(0);
+      }
+      __builtin_amdgcn_sched_barrier(0);   // one tap row's fragments in flight (registers)
+    }
+#pragma unroll
+    for (int yy = 0; yy < SC2_R; ++yy) {
+      const int yo = y0 + yy;
+      if (yo >= H) break;
+      // lane = channel co, registers = pixels (r & 3) + 8 (r >> 2) + 4 h of the segment:
+      // each store instruction writes two 64-B runs (channels 32 nb .. + 31 of two pixels)
+      __bf16* yr = y + ((f * H + yo) * W + sg * 32) * SC2_COUT + co;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int pp = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const __bf16 o = (__bf16)acc[yy][r];
+        if (sg * 32 + pp < W) {
+          const float of = (float)o;
+          s1 += of;
+          s2 = fmaf(of, of, s2);
+          yr[pp * SC2_COUT] = o;
+        }
+      }
+    }
+  }
+  // BN2 partials of this frame: the two halves (same channel), then the 4 segment waves
+  s1 += __shfl_xor(s1, 32, 64);
+  s2 += __shfl_xor(s2, 32, 64);
+  if (h == 0) {
+    red[wv][0][l] = s1;
+    red[wv][1][l] = s2;
+  }
+  __syncthreads();
+  if (t < 2 * SC2_COUT) {
+    const int which = t / SC2_COUT, c = t % SC2_COUT, b3 = c / 32, cl = c % 32;
+    part[(f * 2 + which) * SC2_COUT + c] =
+        ((red[b3][which][cl] + red[3 + b3][which][cl]) + red[6 + b3][which][cl]) + red[9 + b3][which][cl];
   }
 }
 
@@ -1357,6 +1630,57 @@ extern "C" int sm_stem_im2col(int out_dtype, const float* clip, int B, int T, in
                                           stride, (T*)col));
   SM_CHECK_LAUNCH();
   return 0;
+}
+
+// stem conv1 + BN1 statistics (see stem_conv1_kernel); wpack = sm_conv_wpack order 0 [48][32] bf16
+extern "C" int sm_bn_stats_from_partials(const float* part, int64_t nrows, int C, int64_t M, float* mean,
+                                         float* rstd, float* run_mean, float* run_var, int64_t* num_batches_tracked,
+                                         float momentum, float eps, int updates, void* ws, int64_t ws_bytes,
+                                         hipStream_t st);
+extern "C" int64_t sm_stem_conv1_workspace_bytes(void) {
+  return (int64_t)SC1_BLOCKS * 2 * SC1_COUT * 4 + 2 * SC1_COUT * 8 + 64;
+}
+extern "C" int sm_stem_conv1_bn_stats(const float* clip, int B, int T, int H, int W, int64_t sB, int64_t sC,
+                                      int64_t sT, int64_t sH, int64_t sW, const void* wpack, void* y, float* mean,
+                                      float* rstd, float* run_mean, float* run_var, int64_t* num_batches_tracked,
+                                      float momentum, float eps, int updates, void* ws, int64_t ws_bytes,
+                                      hipStream_t st) {
+  ClipView v{clip, B, T, H, W, sB, sC, sT, sH, sW};
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  const int64_t P = (int64_t)B * T * Ho * Wo;
+  if (P <= 0) return 0;
+  if (P >= (1LL << 31) - 64 || (int64_t)3 * sC >= (1LL << 31)) return -2;
+  if (ws_bytes < sm_stem_conv1_workspace_bytes()) return -4;
+  if ((((uintptr_t)wpack) | ((uintptr_t)y)) & 15) return -2;
+  const int64_t nseg = (P + 31) / 32;
+  const int nb = (int)std::min<int64_t>(SC1_BLOCKS, (nseg + 3) / 4);   // part rows
+  float* part = (float*)ws;
+  void* fin = (void*)(((uintptr_t)(part + (int64_t)SC1_BLOCKS * 2 * SC1_COUT) + 15) & ~(uintptr_t)15);
+  hipLaunchKernelGGL(stem_conv1_kernel, dim3(nb), dim3(256), 0, st, v, Ho, Wo, (const __bf16*)wpack, (__bf16*)y, part);
+  SM_CHECK_LAUNCH();
+  return sm_bn_stats_from_partials(part, nb, SC1_COUT, P, mean, rstd, run_mean, run_var, num_batches_tracked,
+                                   momentum, eps, updates, fin, 2 * SC1_COUT * 8, st);
+}
+
+// stem conv2 over GELU(BN1(a1)) + BN2 statistics (see stem_conv2_kernel)
+extern "C" int64_t sm_stem_conv2_workspace_bytes(int F) { return (int64_t)F * 2 * SC2_COUT * 4 + 2 * SC2_COUT * 8 + 64; }
+extern "C" int sm_stem_conv2_bn_stats(const void* a1, int F, int H, int W, const float* bn1_mean,
+                                      const float* bn1_rstd, const float* bn1_w, const float* bn1_b, int gelu,
+                                      const void* wpack, void* y, float* mean, float* rstd, float* run_mean,
+                                      float* run_var, int64_t* num_batches_tracked, float momentum, float eps,
+                                      int updates, void* ws, int64_t ws_bytes, hipStream_t st) {
+  if (F <= 0) return 0;
+  if (H <= 0 || W <= 0 || W > 4 * 32 || (int64_t)F * H * W >= (1LL << 31)) return -2;   // W <= 4 segments
+  if ((((uintptr_t)a1) | ((uintptr_t)wpack) | ((uintptr_t)y)) & 15) return -2;
+  if (ws_bytes < sm_stem_conv2_workspace_bytes(F)) return -4;
+  float* part = (float*)ws;
+  void* fin = (void*)(((uintptr_t)(part + (int64_t)F * 2 * SC2_COUT) + 15) & ~(uintptr_t)15);
+  auto kern = gelu ? stem_conv2_kernel<true> : stem_conv2_kernel<false>;
+  hipLaunchKernelGGL(kern, dim3(F), dim3(SC2_NT), 0, st, (const __bf16*)a1,
+                     ChanAffine{bn1_mean, bn1_rstd, bn1_w, bn1_b, gelu}, (const __bf16*)wpack, (__bf16*)y, part, H, W);
+  SM_CHECK_LAUNCH();
+  return sm_bn_stats_from_partials(part, F, SC2_COUT, (int64_t)F * H * W, mean, rstd, run_mean, run_var,
+                                   num_batches_tracked, momentum, eps, updates, fin, 2 * SC2_COUT * 8, st);
 }
 
 extern "C" int sm_im2col3(int dtype, const void* x, int F, int H, int W, int C, int stride, void* col,

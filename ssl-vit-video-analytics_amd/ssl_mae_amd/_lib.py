@@ -73,6 +73,12 @@ _SIGS = {
     "sm_im2col3": (_c_i32, [_c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p]),
     "sm_col2im3": (_c_i32, [_c_i32, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p]),
     "sm_conv_wpack": (_c_i32, [_c_i32, _c_p, _c_p, _c_i32, _c_i32, _c_i32, _c_i32, _c_p]),
+    "sm_stem_conv1_workspace_bytes": (_c_i64, []),
+    "sm_stem_conv1_bn_stats": (_c_i32, [_c_p] + [_c_i32] * 4 + [_c_i64] * 5 + [_c_p] * 7
+                               + [_c_f32, _c_f32, _c_i32, _c_p, _c_i64, _c_p]),
+    "sm_stem_conv2_workspace_bytes": (_c_i64, [_c_i32]),
+    "sm_stem_conv2_bn_stats": (_c_i32, [_c_p] + [_c_i32] * 3 + [_c_p] * 4 + [_c_i32] + [_c_p] * 7
+                               + [_c_f32, _c_f32, _c_i32, _c_p, _c_i64, _c_p]),
     "sm_conv3x3_fwd": (_c_i32, [_c_p, _c_p, _c_p] + [_c_i32] * 5 + [_c_p]),
     "sm_conv3x3_fwd_bn_stats": (_c_i32, [_c_p, _c_p, _c_p] + [_c_i32] * 5 + [_c_p] * 5
                                 + [_c_f32, _c_f32, _c_i32, _c_p, _c_i64, _c_p]),

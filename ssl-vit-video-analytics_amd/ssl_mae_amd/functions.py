@@ -102,18 +102,27 @@ class StemFn(torch.autograd.Function):
     def forward(ctx, clip, st, w1, g1, b1, w2, g2, b2):
         mode = st.mode
         act = mode.act
-        col1, (Fr, Ho, Wo) = K.stem_im2col(clip, act)
         w1p = K.conv_wpack(w1.detach(), 32, 0, act)
-        if mode.bf16 and st.bn1.training:   # conv1 + BN1 statistics from the GEMM epilogue
-            a1, m1, r1 = K.linear_bn_stats(col1, w1p, st.bn1)
-            del col1
-            h1 = K.bn_apply(a1, m1, r1, g1.detach(), b1.detach(), gelu=True)
+        w2p = K.conv_wpack(w2.detach(), 432, 1, act)
+        h1 = None
+        if mode.bf16 and st.bn1.training:   # conv1 straight from the clip + BN1 statistics
+            a1, m1, r1, (Fr, Ho, Wo) = K.stem_conv1_bn_stats(clip, w1p, st.bn1)
+            if st.bn2.training and Wo <= 128:
+                # conv2 over GELU(BN1(a1)) formed in its LDS ring (h1 never written) + BN2
+                # statistics
+                a2, m2, r2 = K.stem_conv2_bn_stats(a1, (m1, r1, g1.detach(), b1.detach(), True), w2p, Fr, Ho, Wo,
+                                                   st.bn2)
+                y = K.bn_apply(a2, m2, r2, g2.detach(), b2.detach(), gelu=False)
+            else:
+                h1 = K.bn_apply(a1, m1, r1, g1.detach(), b1.detach(), gelu=True)
         else:
+            col1, (Fr, Ho, Wo) = K.stem_im2col(clip, act)
             a1 = K.linear(col1, w1p)
             del col1
             h1, m1, r1 = _bn_forward(a1, st.bn1, gelu=True)
-        w2p = K.conv_wpack(w2.detach(), 432, 1, act)
-        if mode.bf16 and st.bn2.training:   # conv2 as a GEMM over the implicit im2col of h1
+        if h1 is None:
+            pass
+        elif mode.bf16 and st.bn2.training:   # conv2 as a GEMM over the implicit im2col of h1
             # (no 9x buffer) with BN2's statistics from its epilogue (no read pass of a2)
             a2, m2, r2 = K.conv3x3_fwd_bn_stats(h1, w2p, Fr, Ho, Wo, 48, 96, st.bn2)
             del h1

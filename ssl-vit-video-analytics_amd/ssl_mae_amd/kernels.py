@@ -366,6 +366,58 @@ def stem_im2col(clip, out_dtype, frames_view=None):
     return col, (B * T, Ho, Wo)
 
 
+def stem_conv1_bn_stats(clip, wpack, running_mean=None, running_var=None, momentum=0.1, eps=1e-5, updates=1,
+                        num_batches=None):
+    """PatchEmbed conv1 (3->48, 3x3, stride 2, pad 1) straight from the fp32 clip [B,3,T,H,W]
+    (or frames [N,3,H,W]; any strides) with bf16 order-0 packed weights [48][32], plus the
+    train-mode BatchNorm statistics of its bf16 output (sm_stem_conv1_bn_stats;
+    = stem_im2col + linear_bn_stats with no im2col buffer).  Returns (y, mean, rstd, (F, Ho, Wo))."""
+    _chk(clip, wpack)
+    if clip.dtype != torch.float32:
+        clip = clip.float()
+    if wpack.dtype != torch.bfloat16 or tuple(wpack.shape) != (48, 32) or not wpack.is_contiguous():
+        raise _lib.KernelError("stem_conv1_bn_stats: wpack is contiguous bf16 [48][32]")
+    if clip.dim() == 5:
+        B, C, T, H, W = clip.shape
+        sB, sC, sT, sH, sW = clip.stride()
+    else:  # frames [N,3,H,W]
+        B, C, H, W = clip.shape
+        T = 1
+        sB, sC, sH, sW = clip.stride()
+        sT = 0
+    Ho, Wo = (H + 1) // 2, (W + 1) // 2
+    y = torch.empty((B * T * Ho * Wo, 48), dtype=torch.bfloat16, device=clip.device)
+    mean = torch.empty(48, dtype=torch.float32, device=clip.device)
+    rstd = torch.empty(48, dtype=torch.float32, device=clip.device)
+    nbytes = query("sm_stem_conv1_workspace_bytes")
+    ws = _ws(nbytes, clip.device)
+    call("sm_stem_conv1_bn_stats", ptr(clip), B, T, H, W, sB, sC, sT, sH, sW, ptr(wpack), ptr(y), ptr(mean),
+         ptr(rstd), ptr(running_mean), ptr(running_var), ptr(num_batches), float(momentum), float(eps), int(updates),
+         ptr(ws), nbytes, stream())
+    return y, mean, rstd, (B * T, Ho, Wo)
+
+
+def stem_conv2_bn_stats(a1, act, wpack, F, H, W, running_mean=None, running_var=None, momentum=0.1, eps=1e-5,
+                        updates=1, num_batches=None):
+    """PatchEmbed conv2 over h1 = act(a1) (act = (mean, rstd, weight, bias, gelu) of BN1)
+    plus the train-mode BatchNorm statistics of its bf16 output (sm_stem_conv2_bn_stats;
+    = bn_apply + conv3x3_fwd_bn_stats with h1 never written).  a1 [F*H*W, 48] bf16, wpack
+    order-1 [96, 432] bf16.  Returns (y [F*H*W, 96], mean, rstd)."""
+    _chk(a1, wpack)
+    _conv_chk(a1, 48)
+    _conv_chk(wpack, 432)
+    m, r, g, b, gelu = act
+    y = torch.empty((F * H * W, 96), dtype=torch.bfloat16, device=a1.device)
+    mean = torch.empty(96, dtype=torch.float32, device=a1.device)
+    rstd = torch.empty(96, dtype=torch.float32, device=a1.device)
+    nbytes = query("sm_stem_conv2_workspace_bytes", F)
+    ws = _ws(nbytes, a1.device)
+    call("sm_stem_conv2_bn_stats", ptr(a1), F, H, W, ptr(m), ptr(r), ptr(g), ptr(b), int(bool(gelu)), ptr(wpack),
+         ptr(y), ptr(mean), ptr(rstd), ptr(running_mean), ptr(running_var), ptr(num_batches), float(momentum),
+         float(eps), int(updates), ptr(ws), nbytes, stream())
+    return y, mean, rstd
+
+
 def im2col3(x, F, H, W, C, stride):
     Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
     col = torch.empty((F * Ho * Wo, 9 * C), dtype=x.dtype, device=x.device)

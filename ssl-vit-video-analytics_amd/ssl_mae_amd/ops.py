@@ -587,6 +587,65 @@ def conv3x3_fwd(x, wpack, F, H, W, Cin, Cout):
     return torch.ops.ssl_mae.conv3x3_fwd(x, wpack, F, H, W, Cin, Cout)
 
 
+@_op("stem_conv1_bn_stats", "(Tensor clip, Tensor wpack, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
+                            "float momentum, float eps, int updates, Tensor(c!)? num_batches_tracked) "
+                            "-> (Tensor, Tensor, Tensor)",
+     ("running_mean", "running_var", "num_batches_tracked"))
+def _stem_conv1_bn_stats(clip, wpack, running_mean, running_var, momentum, eps, updates, num_batches_tracked):
+    return _K.stem_conv1_bn_stats(clip, wpack, running_mean, running_var, momentum, eps, updates,
+                                  num_batches_tracked)[:3]
+
+
+@_stem_conv1_bn_stats.register_fake
+def _(clip, wpack, *a):
+    if clip.dim() == 5:
+        F, H, W = clip.shape[0] * clip.shape[2], clip.shape[3], clip.shape[4]
+    else:
+        F, H, W = clip.shape[0], clip.shape[2], clip.shape[3]
+    P = F * ((H + 1) // 2) * ((W + 1) // 2)
+    return (clip.new_empty((P, 48), dtype=torch.bfloat16), clip.new_empty(48, dtype=torch.float32),
+            clip.new_empty(48, dtype=torch.float32))
+
+
+def stem_conv1_bn_stats(clip, wpack, bn, updates=1):
+    """Stem conv1 from the clip + the train-mode statistics of its BatchNorm (no im2col buffer).
+    Returns (y, mean, rstd, (F, Ho, Wo))."""
+    if clip.dim() == 5:
+        F, H, W = clip.shape[0] * clip.shape[2], clip.shape[3], clip.shape[4]
+    else:
+        F, H, W = clip.shape[0], clip.shape[2], clip.shape[3]
+    y, m, r = torch.ops.ssl_mae.stem_conv1_bn_stats(clip, wpack, bn.running_mean, bn.running_var,
+                                                    float(bn.momentum), float(bn.eps), int(updates),
+                                                    bn.num_batches_tracked)
+    return y, m, r, (F, (H + 1) // 2, (W + 1) // 2)
+
+
+@_op("stem_conv2_bn_stats", "(Tensor a1, Tensor bn1_mean, Tensor bn1_rstd, Tensor bn1_w, Tensor bn1_b, bool gelu, "
+                            "Tensor wpack, int F, int H, int W, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
+                            "float momentum, float eps, int updates, Tensor(c!)? num_batches_tracked) "
+                            "-> (Tensor, Tensor, Tensor)",
+     ("running_mean", "running_var", "num_batches_tracked"))
+def _stem_conv2_bn_stats(a1, m, r, g, b, gelu, wpack, F, H, W, running_mean, running_var, momentum, eps, updates,
+                         num_batches_tracked):
+    return _K.stem_conv2_bn_stats(a1, (m, r, g, b, gelu), wpack, F, H, W, running_mean, running_var, momentum, eps,
+                                  updates, num_batches_tracked)
+
+
+@_stem_conv2_bn_stats.register_fake
+def _(a1, m, r, g, b, gelu, wpack, F, H, W, *a):
+    return (a1.new_empty((F * H * W, 96), dtype=torch.bfloat16), a1.new_empty(96, dtype=torch.float32),
+            a1.new_empty(96, dtype=torch.float32))
+
+
+def stem_conv2_bn_stats(a1, act, wpack, F, H, W, bn, updates=1):
+    """Stem conv2 over act(a1) (BN1 + GELU applied on the fly, h1 never written) + the
+    train-mode statistics of BN2."""
+    m, r, g, b, gelu = act
+    return torch.ops.ssl_mae.stem_conv2_bn_stats(a1, m, r, g, b, bool(gelu), wpack, F, H, W, bn.running_mean,
+                                                 bn.running_var, float(bn.momentum), float(bn.eps), int(updates),
+                                                 bn.num_batches_tracked)
+
+
 @_op("conv3x3_fwd_bn_stats", "(Tensor x, Tensor wpack, int F, int H, int W, int Cin, int Cout, "
                              "Tensor(a!)? running_mean, Tensor(b!)? running_var, float momentum, float eps, "
                              "int updates, Tensor(c!)? num_batches_tracked) -> (Tensor, Tensor, Tensor)",

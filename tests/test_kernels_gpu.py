@@ -816,6 +816,64 @@ def test_linear_bn_stats(M, N, Kd, upd):
     assert rel_err(r2, 1.0 / torch.sqrt(yf.var(0, unbiased=False) + 1e-5)) < 1e-4
 
 
+@pytest.mark.parametrize("shape,frames", [((2, 3, 3, 37, 30), False), ((1, 3, 8, 224, 224), False),
+                                          ((5, 3, 17, 23), True), ((32, 3, 8, 224, 224), False)])
+def test_stem_conv1_direct(shape, frames):
+    """Stem conv1 straight from the strided fp32 clip (sm_stem_conv1_bn_stats): a1
+    bit-identical to stem_im2col + linear_bn_stats (the same MFMA products and order),
+    BN1 statistics / running statistics within fp32 rounding of the GEMM epilogue's.
+    Shapes: odd frame sizes (Ho = 19, Wo = 15: pixel segments straddle rows), one full
+    clip, a frames view [N,3,H,W] with a non-contiguous layout, B = 32 clips at 224^2."""
+    kk = KK()
+    g = torch.Generator().manual_seed(220)
+    if frames:
+        clip = torch.randn(shape[0], shape[2], shape[3], shape[1], generator=g).to(DEV).permute(0, 3, 1, 2)
+    else:
+        clip = torch.randn(*shape, generator=g).to(DEV)
+    wp = kk.conv_wpack((torch.randn(48, 3, 3, 3, generator=g) * 0.2).to(DEV), 32, 0, torch.bfloat16)
+    rm1, rv1 = torch.full((48,), 0.1, device=DEV), torch.full((48,), 2.0, device=DEV)
+    rm2, rv2 = rm1.clone(), rv1.clone()
+    nb1 = torch.zeros((), dtype=torch.int64, device=DEV)
+    nb2 = nb1.clone()
+    col, geom1 = kk.stem_im2col(clip, torch.bfloat16)
+    y1, m1, r1 = kk.linear_bn_stats(col, wp, rm1, rv1, 0.1, 1e-5, 1, nb1)
+    y2, m2, r2, geom2 = kk.stem_conv1_bn_stats(clip, wp, rm2, rv2, 0.1, 1e-5, 1, nb2)
+    assert geom1 == geom2
+    assert torch.equal(y1, y2)
+    assert rel_err(m2, m1) < 1e-5 and rel_err(r2, r1) < 1e-5
+    assert rel_err(rm2, rm1) < 1e-5 and rel_err(rv2, rv1) < 1e-5
+    assert int(nb2) == 1 == int(nb1)
+
+
+@pytest.mark.parametrize("Fn,H,W,gelu", [(3, 14, 12, True), (2, 9, 23, True), (32, 112, 112, True),
+                                         (1, 5, 128, True), (2, 1, 7, False), (3, 3, 33, False)])
+def test_stem_conv2_direct(Fn, H, W, gelu):
+    """Stem conv2 over act(a1) with BN1 (+GELU) applied in the kernel's LDS ring
+    (sm_stem_conv2_bn_stats): y bit-identical to conv3x3_fwd(bn_apply(a1)) (same k order
+    and MFMA chain), BN2 statistics / running statistics within fp32 rounding.  Shapes:
+    ragged pixel segments (W = 12, 23, 33), the bench frame (112^2, 32 frames), the widest
+    frame (W = 128), a single row (H = 1), odd band counts; identity activation."""
+    kk = KK()
+    g = torch.Generator().manual_seed(230)
+    a1 = (torch.randn(Fn * H * W, 48, generator=g) * 2).to(torch.bfloat16).to(DEV)
+    m1 = (torch.randn(48, generator=g) * 0.3).to(DEV)
+    r1 = (torch.rand(48, generator=g) + 0.5).to(DEV)
+    g1 = (torch.rand(48, generator=g) + 0.5).to(DEV)
+    b1 = (torch.randn(48, generator=g) * 0.1).to(DEV)
+    wp = kk.conv_wpack((torch.randn(96, 48, 3, 3, generator=g) * 0.05).to(DEV), 432, 1, torch.bfloat16)
+    rm1, rv1 = torch.full((96,), 0.1, device=DEV), torch.full((96,), 2.0, device=DEV)
+    rm2, rv2 = rm1.clone(), rv1.clone()
+    nb1 = torch.zeros((), dtype=torch.int64, device=DEV)
+    nb2 = nb1.clone()
+    h1 = kk.bn_apply(a1, m1, r1, g1, b1, gelu=gelu)
+    y1, mm1, rr1 = kk.conv3x3_fwd_bn_stats(h1, wp, Fn, H, W, 48, 96, rm1, rv1, 0.1, 1e-5, 1, nb1)
+    y2, mm2, rr2 = kk.stem_conv2_bn_stats(a1, (m1, r1, g1, b1, gelu), wp, Fn, H, W, rm2, rv2, 0.1, 1e-5, 1, nb2)
+    assert torch.equal(y1, y2)
+    assert rel_err(mm2, mm1) < 1e-5 and rel_err(rr2, rr1) < 1e-5
+    assert rel_err(rm2, rm1) < 1e-5 and rel_err(rv2, rv1) < 1e-5
+    assert int(nb2) == 1 == int(nb1)
+
+
 @pytest.mark.parametrize("Fn,H,W,Cin,Cout,upd", [(3, 14, 12, 48, 96, 1), (2, 9, 23, 16, 24, 2),
                                                   (32, 112, 112, 48, 96, 1), (1, 3, 5, 8, 8, 1)])
 def test_conv3x3_fwd_bn_stats(Fn, H, W, Cin, Cout, upd):
