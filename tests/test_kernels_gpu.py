@@ -129,7 +129,7 @@ def _attn_ref(qkv, N, L, H, D):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("D", [32, 64])
-@pytest.mark.parametrize("L", [50, 128, 200])
+@pytest.mark.parametrize("L", [50, 128, 150, 200])
 def test_attention_fwd_bwd(dtype, D, L):
     N, H = 2, 3
     qkv = rnd(N * L, 3 * H * D, dtype=dtype, seed=20 + L + D)
