@@ -245,6 +245,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(AttnArgs a) {
   const __bf16* kb = qkv + C + hd * D;
   const __bf16* vb = qkv + 2 * C + hd * D;
   const int q = tl.qb * 128 + w * 32 + (l & 31);
+  // a wave whose 32 query rows all lie past L (the last block of a (sample, head) when L
+  // is not a multiple of 128: 3.5 of 4 waves at L = 784) only helps stage the tiles
+  const bool wact = tl.qb * 128 + w * 32 < a.L;
 
   bf16x8 qf[D / 16];
 #pragma unroll
@@ -287,11 +290,16 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(AttnArgs a) {
       stg.load(kb + (int64_t)(k0 + KT) * ldq, a.L - k0 - KT, rk);
       stg.load(vb + (int64_t)(k0 + KT) * ldq, a.L - k0 - KT, rv);
     }
+    if (!wact) return;
+    // ragged tile: the second 32-key half has no key below L when <= 32 keys remain (its
+    // scores are masked to -inf below either way): no MFMAs for it
+    const bool half1 = !RAGGED || k0 + 32 < a.L;
     f32x16 st[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) st[u][r] = 0.f;
+      if (u == 1 && !half1) continue;
 #pragma unroll
       for (int s = 0; s < D / 16; ++s)
         st[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_b128(lk, koff[s] + u * RB), qf[s], st[u], 0, 0, 0);
@@ -348,6 +356,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(AttnArgs a) {
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
+        if (u == 1 && !half1) continue;   // P = 0 there
         const bf16x8 pf = __builtin_bit_cast(
             bf16x8, make_uint4(pw[u][2 * s][0], pw[u][2 * s][1], pw[u][2 * s + 1][0], pw[u][2 * s + 1][1]));
 #pragma unroll
@@ -425,6 +434,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(AttnArgs a) {
   const float* lse = a.lse + ((int64_t)n * a.H + hd) * a.L;
   const float* del = a.delta + ((int64_t)n * a.H + hd) * a.L;
   const int key = tl.qb * 128 + w * 32 + (l & 31);
+  const bool wact = tl.qb * 128 + w * 32 < a.L;   // else: only stages tiles (see the forward)
 
   bf16x8 kf[D / 16], vf[D / 16];
 #pragma unroll
@@ -548,6 +558,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(AttnArgs a) {
       sq.load(qb + (int64_t)(q0 + QT) * ldq, a.L - q0 - QT, rq);
       sd.load(dob + (int64_t)(q0 + QT) * C, a.L - q0 - QT, rd);
     }
+    if (!wact) continue;
     f32x16 s0, p0, s1, p1;
     bf16x8 pf0[2], sf0[2], pf1[2], sf1[2];
     sdp(0, s0, p0);
@@ -592,6 +603,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16(AttnArgs a) {
   const __bf16* dob = (const __bf16*)a.dout + (int64_t)n * a.L * C + hd * D;
   const int q = tl.qb * 128 + w * 32 + (l & 31);
   const bool qok = q < a.L;
+  const bool wact = tl.qb * 128 + w * 32 < a.L;   // else: only stages tiles (see the forward)
   const float lse2 = qok ? a.lse[((int64_t)n * a.H + hd) * a.L + q] * LOG2E : 1e30f;
 
   // This lane's half of dO's and O's row for query q (D/2 values): Delta = rowsum(dO*O)
@@ -650,8 +662,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16(AttnArgs a) {
       stg.load(kb + (int64_t)(k0 + KT) * ldq, a.L - k0 - KT, rk);
       stg.load(vb + (int64_t)(k0 + KT) * ldq, a.L - k0 - KT, rv);
     }
+    if (!wact) return;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
+      if (RAGGED && u == 1 && k0 + 32 >= a.L) continue;   // no key below L in this half
       f32x16 sacc, dpacc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) { sacc[r] = -lse2; dpacc[r] = 0.f; }
