@@ -172,6 +172,26 @@ def gemmk(args):
         torch.cuda.empty_cache()
 
 
+def gemmw(args):
+    """Write-rate probe: the stage-0 expand shape (M = batch*8*112^2 rows, N = 384 bf16 out)
+    at tiny K against a plain fill of the same output."""
+    M, N = args.batch * 8 * 12544, 384
+    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    gbw = M * N * 2 / 1e9
+    t = timeit(lambda: out.zero_(), args.iters)
+    print(f"fill [M={M}, {N}] bf16: {t:7.3f} ms  {gbw / t:6.2f} TB/s written", flush=True)
+    del out
+    for Kd in (8, 32, 96):
+        x = torch.randn(M, Kd, device="cuda").to(torch.bfloat16)
+        w = torch.randn(N, Kd, device="cuda").to(torch.bfloat16)
+        t = timeit(lambda: K.linear(x, w), args.iters)
+        gbr = M * Kd * 2 / 1e9
+        print(f"linear M={M} N={N} K={Kd}: {t:7.3f} ms  {gbw / t:6.2f} TB/s written, {gbr / t:6.2f} read",
+              flush=True)
+        del x, w
+        torch.cuda.empty_cache()
+
+
 def stem(args):
     """PatchEmbed forward pieces at B clips of 8x224^2 (bf16), HIP-event timed."""
     dev = "cuda"
@@ -253,7 +273,7 @@ def mbconv(args):
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["attn", "gemm", "gemmk", "mbconv", "dw", "dwx", "dwse", "stem"])
+    ap.add_argument("what", choices=["attn", "gemm", "gemmk", "mbconv", "dw", "dwx", "dwse", "stem", "gemmw"])
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--drop", type=float, default=0.1)
     ap.add_argument("--iters", type=int, default=5)
@@ -261,4 +281,4 @@ if __name__ == "__main__":
     a = ap.parse_args()
     from ssl_mae_amd.build import build
     build()
-    {"attn": attn, "gemm": gemm, "gemmk": gemmk, "mbconv": mbconv, "dw": dw, "dwx": dwx, "dwse": dwse, "stem": stem}[a.what](a)
+    {"attn": attn, "gemm": gemm, "gemmk": gemmk, "mbconv": mbconv, "dw": dw, "dwx": dwx, "dwse": dwse, "stem": stem, "gemmw": gemmw}[a.what](a)
