@@ -229,12 +229,22 @@ SM_DEV bf16x8 lds_tr(const char* lds, int lo, int hi) {
 }
 
 // =============================================================== bf16 forward
+// Softmax without a running maximum.  Q is pre-scaled by scale*log2(e) once in registers,
+// so the MFMA leaves the exp2 argument itself and the fast pass computes P = exp2(S) with
+// no maximum, no subtraction and no rescale of O (softmax is shift-invariant and fp32 /
+// bf16 keep their relative precision at any scale: only the exponent range matters).  Per
+// score that leaves the exp, the row-sum add and half a bf16 pack (the online-softmax form
+// also spent a max, an fma and the rescale bookkeeping: ~45 % of the d = 32 loop's VALU).
+// A row whose sum leaves [2^-100, 2^100] or whose O is not finite (scores beyond the
+// exponent range: |S| > ~100 in log2 units) makes the block rerun the whole key loop with
+// the online (max-tracking) softmax, so results never depend on the fast pass's range.
 template <int D, bool DROP>
 __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(AttnArgs a) {
   constexpr int KT = 64;
   constexpr int RB = 32 * D * 2;   // bytes of 32 tile rows
   __shared__ __attribute__((aligned(16))) char lk[KT * D * 2];
   __shared__ __attribute__((aligned(16))) char lv[KT * D * 2];
+  __shared__ int lbad;
   const AttnTile tl((a.L + 127) / 128, a.H);
   const int n = tl.n, hd = tl.hd;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5;
@@ -248,12 +258,16 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(AttnArgs a) {
   // a wave whose 32 query rows all lie past L (the last block of a (sample, head) when L
   // is not a multiple of 128: 3.5 of 4 waves at L = 784) only helps stage the tiles
   const bool wact = tl.qb * 128 + w * 32 < a.L;
+  if (threadIdx.x == 0) lbad = 0;   // ordered before any write by the first tile's barriers
 
+  const float c = a.scale * LOG2E;
   bf16x8 qf[D / 16];
 #pragma unroll
   for (int s = 0; s < D / 16; ++s) {
     if (q < a.L) qf[s] = *(const bf16x8*)(qb + (int64_t)q * ldq + 16 * s + 8 * h);
     else for (int j = 0; j < 8; ++j) qf[s][j] = (__bf16)0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qf[s][j] = (__bf16)((float)qf[s][j] * c);
   }
   Stager<D, KT> stg;
   stg.init(ldq);
@@ -264,111 +278,132 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(AttnArgs a) {
   for (int t = 0; t < D / 32; ++t) tr_frag_off<D>(t, vlo[t], vhi[t]);
 
   f32x16 o[D / 32];
-#pragma unroll
-  for (int t = 0; t < D / 32; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) o[t][r] = 0.f;
-  float m = NEG_BIG, lsum = 0.f;
-  const float c = a.scale * LOG2E;
+  float m = 0.f, lsum = 0.f;
   // hash input minus its wave-uniform column part: row term + this half's group
   const uint32_t dlb = seed32(a.seed) + (uint32_t)((uint64_t)(n * a.H + hd) * a.L + q) * AG + (uint32_t)h * AC;
   const uint32_t dthr = attn_thr(a.drop_p);
 
   uint4 rk[Stager<D, KT>::CH], rv[Stager<D, KT>::CH];
-  stg.load(kb, a.L, rk);
-  stg.load(vb, a.L, rv);
-  // one key tile; the ragged last tile is its own instantiation: the compiler turned the
-  // uniform `if (ragged)` key-range masking into per-element selects executed on EVERY
-  // tile (~80 VALU per tile of the d=32 kernels)
-  auto tile = [&](int k0, auto rag) {
-    constexpr bool RAGGED = decltype(rag)::value;
-    __syncthreads();
-    stg.store(lk, rk);
-    stg.store(lv, rv);
-    __syncthreads();
-    if (k0 + KT < a.L) {                       // prefetch the next tile under this tile's math
-      stg.load(kb + (int64_t)(k0 + KT) * ldq, a.L - k0 - KT, rk);
-      stg.load(vb + (int64_t)(k0 + KT) * ldq, a.L - k0 - KT, rv);
-    }
-    if (!wact) return;
-    // ragged tile: the second 32-key half has no key below L when <= 32 keys remain (its
-    // scores are masked to -inf below either way): no MFMAs for it
-    const bool half1 = !RAGGED || k0 + 32 < a.L;
-    f32x16 st[2];
+  // one pass over the keys; SAFE: online softmax with the running maximum m
+  auto pass = [&](auto safe) {
+    constexpr bool SAFE = decltype(safe)::value;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int t = 0; t < D / 32; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) st[u][r] = 0.f;
-      if (u == 1 && !half1) continue;
+      for (int r = 0; r < 16; ++r) o[t][r] = 0.f;
+    m = SAFE ? NEG_BIG : 0.f;
+    lsum = 0.f;
+    stg.load(kb, a.L, rk);
+    stg.load(vb, a.L, rv);
+    // one key tile; the ragged last tile is its own instantiation: the compiler turned the
+    // uniform `if (ragged)` key-range masking into per-element selects executed on EVERY
+    // tile (~80 VALU per tile of the d=32 kernels)
+    auto tile = [&](int k0, auto rag) {
+      constexpr bool RAGGED = decltype(rag)::value;
+      __syncthreads();
+      stg.store(lk, rk);
+      stg.store(lv, rv);
+      __syncthreads();
+      if (k0 + KT < a.L) {                       // prefetch the next tile under this tile's math
+        stg.load(kb + (int64_t)(k0 + KT) * ldq, a.L - k0 - KT, rk);
+        stg.load(vb + (int64_t)(k0 + KT) * ldq, a.L - k0 - KT, rv);
+      }
+      if (!wact) return;
+      // ragged tile: the second 32-key half has no key below L when <= 32 keys remain (its
+      // scores are masked to -inf below either way): no MFMAs for it
+      const bool half1 = !RAGGED || k0 + 32 < a.L;
+      f32x16 st[2];
 #pragma unroll
-      for (int s = 0; s < D / 16; ++s)
-        st[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_b128(lk, koff[s] + u * RB), qf[s], st[u], 0, 0, 0);
-    }
-    // raw-score max (scale > 0 keeps the argmax); masking only on the ragged tile
-    if constexpr (RAGGED) {
+      for (int u = 0; u < 2; ++u) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) st[u][r] = 0.f;
+        if (u == 1 && !half1) continue;
+#pragma unroll
+        for (int s = 0; s < D / 16; ++s)
+          st[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_b128(lk, koff[s] + u * RB), qf[s], st[u], 0, 0, 0);
+      }
+      if constexpr (RAGGED) {   // keys past L: P = exp2(-huge) = 0
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (k0 + 32 * u + acc_row(r, h) >= a.L) st[u][r] = NEG_BIG;
+      }
+      float alpha = 1.f, mn = 0.f;
+      bool grow = false;
+      if constexpr (SAFE) {
+        float mt = NEG_BIG;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) mt = fmaxf(mt, st[u][r]);
+        mt = halves_max(mt);
+        // rescale only when some row's max grew (exact: alpha == 1 otherwise)
+        grow = mt > m;
+        mn = grow ? mt : m;
+        alpha = grow ? __builtin_amdgcn_exp2f(m - mn) : 1.f;
+        m = mn;
+      }
+      float ps = 0.f;
+      uint32_t pw[2][4][2];   // bf16 pairs of P (dropout applied): [u][g][keys 4g+0,1 | 4g+2,3]
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          float p4[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            p4[j] = __builtin_amdgcn_exp2f(SAFE ? st[u][4 * g + j] - mn : st[u][4 * g + j]);
+            ps += p4[j];
+          }
+          uint32_t w0 = pack_bf16x2(p4[0], p4[1]), w1 = pack_bf16x2(p4[2], p4[3]);
+          if (DROP) {   // keys k0+32u+8g+4h+j, j = 0..3, share one hash; masks on the packed pairs
+            const uint32_t y = keep_flags(mix24(dlb + (uint32_t)((k0 >> 2) + 8 * u + 2 * g) * AC), dthr);
+            w0 &= keep_mask01(y);
+            w1 &= keep_mask23(y);
+          }
+          pw[u][g][0] = w0;
+          pw[u][g][1] = w1;
+        }
+      }
+      if constexpr (SAFE) {
+        lsum = lsum * alpha + ps;
+        if (__any(grow)) {
+#pragma unroll
+          for (int t = 0; t < D / 32; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+        }
+      } else {
+        lsum += ps;
+      }
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (k0 + 32 * u + acc_row(r, h) >= a.L) st[u][r] = NEG_BIG;
-    }
-    float mt = NEG_BIG;
+        for (int s = 0; s < 2; ++s) {
+          if (u == 1 && !half1) continue;   // P = 0 there
+          const bf16x8 pf = __builtin_bit_cast(
+              bf16x8, make_uint4(pw[u][2 * s][0], pw[u][2 * s][1], pw[u][2 * s + 1][0], pw[u][2 * s + 1][1]));
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) mt = fmaxf(mt, st[u][r]);
-    mt = halves_max(mt) * c;
-    // rescale only when some row's max grew (exact: alpha == 1 otherwise)
-    const bool grow = mt > m;
-    const float mn = grow ? mt : m;
-    const float alpha = grow ? __builtin_amdgcn_exp2f(m - mn) : 1.f;
-    m = mn;
-    float ps = 0.f;
-    uint32_t pw[2][4][2];   // bf16 pairs of P (dropout applied): [u][g][keys 4g+0,1 | 4g+2,3]
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        float p4[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          p4[j] = __builtin_amdgcn_exp2f(fmaf(st[u][4 * g + j], c, -mn));
-          ps += p4[j];
+          for (int t = 0; t < D / 32; ++t)
+            o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                lds_tr(lv, vlo[t] + u * RB + s * (RB / 2), vhi[t] + u * RB + s * (RB / 2)), pf, o[t], 0, 0, 0);
         }
-        uint32_t w0 = pack_bf16x2(p4[0], p4[1]), w1 = pack_bf16x2(p4[2], p4[3]);
-        if (DROP) {   // keys k0+32u+8g+4h+j, j = 0..3, share one hash; masks on the packed pairs
-          const uint32_t y = keep_flags(mix24(dlb + (uint32_t)((k0 >> 2) + 8 * u + 2 * g) * AC), dthr);
-          w0 &= keep_mask01(y);
-          w1 &= keep_mask23(y);
-        }
-        pw[u][g][0] = w0;
-        pw[u][g][1] = w1;
-      }
-    }
-    lsum = lsum * alpha + ps;
-    if (__any(grow)) {
-#pragma unroll
-      for (int t = 0; t < D / 32; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        if (u == 1 && !half1) continue;   // P = 0 there
-        const bf16x8 pf = __builtin_bit_cast(
-            bf16x8, make_uint4(pw[u][2 * s][0], pw[u][2 * s][1], pw[u][2 * s + 1][0], pw[u][2 * s + 1][1]));
-#pragma unroll
-        for (int t = 0; t < D / 32; ++t)
-          o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-              lds_tr(lv, vlo[t] + u * RB + s * (RB / 2), vhi[t] + u * RB + s * (RB / 2)), pf, o[t], 0, 0, 0);
-      }
+    };
+    int k0 = 0;
+    for (; k0 + KT <= a.L; k0 += KT) tile(k0, std::false_type{});
+    if (k0 < a.L) tile(k0, std::true_type{});
+    lsum = halves_sum(lsum);
   };
-  int k0 = 0;
-  for (; k0 + KT <= a.L; k0 += KT) tile(k0, std::false_type{});
-  if (k0 < a.L) tile(k0, std::true_type{});
-  lsum = halves_sum(lsum);
+  pass(std::false_type{});
+  bool bad = !(lsum >= 0x1p-100f && lsum <= 0x1p100f);
+#pragma unroll
+  for (int t = 0; t < D / 32; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) bad |= !__builtin_isfinite(o[t][r]);
+  if (wact && __any(bad && q < a.L) && l == 0) lbad = 1;
+  __syncthreads();
+  if (lbad) pass(std::true_type{});   // block-uniform: the rerun's barriers are safe
   if (q < a.L) {
     const float inv = (DROP ? 1.f / (1.f - a.drop_p) : 1.f) / lsum;
     __bf16* ob = (__bf16*)a.out + ((int64_t)n * a.L + q) * C + hd * D;

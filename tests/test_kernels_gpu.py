@@ -148,6 +148,41 @@ def test_attention_fwd_bwd(dtype, D, L):
     assert rel_err(dqkv, dqkv_ref) < (1e-4 if dtype == torch.float32 else 3e-2)
 
 
+@pytest.mark.parametrize("D", [32, 64])
+@pytest.mark.parametrize("case", ["overflow", "underflow"])
+def test_attention_fwd_outside_fast_range(D, case):
+    """The bf16 forward's max-free pass (P = exp2(S), Q pre-scaled by scale*log2 e) is
+    only valid while every row sum stays in [2^-100, 2^100]; rows beyond it must make
+    their block rerun with the online softmax.  overflow: sample 0's q, k scaled so the
+    log2 scores reach ~150 (sample 1 stays on the fast pass); underflow: every score of
+    a row below -130 (q = a u, k = -a u).  Reference: fp32 softmax over the same
+    bf16(q * scale * log2 e) scores."""
+    N, L, H = 2, 200, 3
+    g = torch.Generator().manual_seed(70 + D)
+    x = torch.randn(N * L, 3 * H * D, generator=g)
+    if case == "overflow":
+        x[:L, :2 * H * D] *= 6.0
+    else:
+        u = torch.randn(H * D, generator=g)
+        x[:, :H * D] = 5.0 * u + 0.5 * x[:, :H * D]
+        x[:, H * D:2 * H * D] = -5.0 * u + 0.5 * x[:, H * D:2 * H * D]
+    qkv = x.to(torch.bfloat16)
+    q, k, v = qkv.float().reshape(N, L, 3, H, D).permute(2, 0, 3, 1, 4)
+    c = math.log2(math.e) / math.sqrt(D)
+    s2 = (q * c).to(torch.bfloat16).float() @ k.transpose(-1, -2)   # log2 units
+    o_ref = torch.softmax(s2 * math.log(2.0), -1) @ v
+    o_ref_flat = o_ref.transpose(1, 2).reshape(N * L, H * D)
+    lse_ref = torch.logsumexp(s2 * math.log(2.0), -1)
+    if case == "overflow":
+        assert s2[0].max() > 128   # the fast pass overflows here
+    else:
+        assert s2.max() < -100     # and underflows here
+    o, lse = KK().attn_fwd(qkv.to(DEV), N, L, H, D)
+    assert torch.isfinite(o.float()).all()
+    assert rel_err(o, o_ref_flat) < TOL[torch.bfloat16]
+    assert rel_err(lse, lse_ref) < 1e-3
+
+
 def test_attention_dropout_statistics():
     """Dropout on P: E[O] unchanged; the same seed gives the same output."""
     N, L, H, D = 1, 256, 2, 64
