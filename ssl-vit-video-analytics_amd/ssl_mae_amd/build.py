@@ -22,7 +22,7 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", CSRC, "-I
 # Per-source extra flags.  fed.hip reproduces the reference's separately rounded
 # multiply and add bit for bit; hipcc's default -ffp-contract=fast ignores
 # `#pragma clang fp contract`, so contraction is switched off for that file.
-FILE_FLAGS = {"fed.hip": ["-ffp-contract=off"]}
+FILE_FLAGS = {"fed.hip": ["-ffp-contract=off"], "attention.hip": ["-fno-slp-vectorize"]}
 
 
 def _sources():
