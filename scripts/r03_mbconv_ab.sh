@@ -1,0 +1,11 @@
+# depthwise / MBConv kernel tests on this tree + same-box kbench A/B of the stage-0 MBConv
+# streaming kernels: ab_base/ (baseline worktree with its own library) vs this tree, twice
+set -e
+TAG=${1:-r03w}
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py tests/test_c2_bf16_gpu.py -m gpu -k "dw or mbconv or MBConv" > gpurun_out/${TAG}_tests.log 2>&1
+for i in 1 2; do
+(cd ab_base && timeout -k 10 300 python scripts/kbench.py mbconv --iters 5) > gpurun_out/${TAG}_kb_base$i.log 2>&1
+timeout -k 10 300 python scripts/kbench.py mbconv --iters 5 > gpurun_out/${TAG}_kb_new$i.log 2>&1
+done

@@ -908,6 +908,11 @@ __global__ __launch_bounds__(256, 2) void dwb_kernel(const __bf16* dy, const __b
   const int nstrip = (W + PX - 1) / PX;
   const int items = TY * nstrip;
   const int nbands = (H + TY - 1) / TY;
+  // frame-level views of x and dz (wave-uniform descriptors: a per-row descriptor built from
+  // each thread's item is divergent, and every buffer access through it became a waterfall
+  // loop of up to 8 passes)
+  const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)(x + f * H * W * C), (short)0, H * W * C * 2, 0x00020000);
+  const auto zr = __builtin_amdgcn_make_buffer_rsrc((void*)(dz + f * H * W * C), (short)0, H * W * C * 2, 0x00020000);
   ring.stage_first<true>(lds, raw);
   for (int band = 0; band < nbands; ++band) {
     const int y0 = band * TY;
@@ -924,10 +929,11 @@ __global__ __launch_bounds__(256, 2) void dwb_kernel(const __bf16* dy, const __b
       if (yi >= H) continue;
       const int xi0 = strip * PX;
       // this pixel row of x and dz as buffer views: pixels past W read 0 / drop stores
-      const int64_t row0 = (f * H + yi) * W;
-      const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)(x + row0 * C), (short)0, W * C * 2, 0x00020000);
-      const auto zr = __builtin_amdgcn_make_buffer_rsrc((void*)(dz + row0 * C), (short)0, W * C * 2, 0x00020000);
-      const uint32_t off0 = (uint32_t)(xi0 * C + c0) * 2u;
+      // pixels past W: out-of-range offset (loads read 0, stores are dropped)
+      const uint32_t off0 = (uint32_t)((yi * W + xi0) * C + c0) * 2u;
+      uint32_t offp[PX];
+#pragma unroll
+      for (int p = 0; p < PX; ++p) offp[p] = xi0 + p < W ? off0 + (uint32_t)(p * C * 2) : 0x80000000u;
       float h[PX][4], gg[PX][4], g[PX][4];
       bf16x4 xs[PX];                     // x itself (xhat is formed after the tap loop)
       {
@@ -936,7 +942,7 @@ __global__ __launch_bounds__(256, 2) void dwb_kernel(const __bf16* dy, const __b
         load4(cl + DWF_CB + c4 * 4, sh);
 #pragma unroll
         for (int p = 0; p < PX; ++p)
-          xs[p] = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(xr, off0 + p * C * 2, 0, 0));
+          xs[p] = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(xr, offp[p], 0, 0));
 #pragma unroll
         for (int p = 0; p < PX; ++p) {
           const bool ok = xi0 + p < W;
@@ -999,7 +1005,7 @@ __global__ __launch_bounds__(256, 2) void dwb_kernel(const __bf16* dy, const __b
         bf16x4 o;
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[j] = (__bf16)d[j];
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, o), zr, off0 + p * C * 2, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, o), zr, offp[p], 0, 0);
       }
     }
   }
@@ -1081,6 +1087,9 @@ __global__ __launch_bounds__(256, 2) void dwb2_kernel(const __bf16* dy, const __
   const int nstrip = (W + PX - 1) / PX;
   const int items = TYI * nstrip;
   const int nbands = (H + TYI - 1) / TYI;
+  // frame-level views of x and dz (wave-uniform descriptors; see dwb_kernel)
+  const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)(x + f * H * W * C), (short)0, H * W * C * 2, 0x00020000);
+  const auto zr = __builtin_amdgcn_make_buffer_rsrc((void*)(dz + f * H * W * C), (short)0, H * W * C * 2, 0x00020000);
   ring.stage_first<true>(lds, raw);
   for (int band = 0; band < nbands; ++band) {
     const int y0 = band * TYI, yo0 = band * DWB2_TYO;
@@ -1096,10 +1105,11 @@ __global__ __launch_bounds__(256, 2) void dwb2_kernel(const __bf16* dy, const __
       const int yi = y0 + ry;
       if (yi >= H) continue;
       const int xi0 = strip * PX;
-      const int64_t row0 = (f * H + yi) * W;
-      const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)(x + row0 * C), (short)0, W * C * 2, 0x00020000);
-      const auto zr = __builtin_amdgcn_make_buffer_rsrc((void*)(dz + row0 * C), (short)0, W * C * 2, 0x00020000);
-      const uint32_t off0 = (uint32_t)(xi0 * C + c0) * 2u;
+      // pixels past W: out-of-range offset (loads read 0, stores are dropped)
+      const uint32_t off0 = (uint32_t)((yi * W + xi0) * C + c0) * 2u;
+      uint32_t offp[PX];
+#pragma unroll
+      for (int p = 0; p < PX; ++p) offp[p] = xi0 + p < W ? off0 + (uint32_t)(p * C * 2) : 0x80000000u;
       float h[PX][4], gg[PX][4], g[PX][4];
       bf16x4 xs[PX];
       {
@@ -1108,7 +1118,7 @@ __global__ __launch_bounds__(256, 2) void dwb2_kernel(const __bf16* dy, const __
         load4(cl + DWF_CB + c4 * 4, sh);
 #pragma unroll
         for (int p = 0; p < PX; ++p)
-          xs[p] = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(xr, off0 + p * C * 2, 0, 0));
+          xs[p] = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(xr, offp[p], 0, 0));
 #pragma unroll
         for (int p = 0; p < PX; ++p) {
           const bool ok = xi0 + p < W;
@@ -1178,7 +1188,7 @@ __global__ __launch_bounds__(256, 2) void dwb2_kernel(const __bf16* dy, const __
         bf16x4 o;
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[j] = (__bf16)d[j];
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, o), zr, off0 + p * C * 2, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_t, o), zr, offp[p], 0, 0);
       }
     }
   }
