@@ -863,7 +863,9 @@ __global__ __launch_bounds__(256, 2) void dwf_wgrad_kernel(const __bf16* dy, con
 constexpr int DWB_PX = 7, DWB_PAD = 8 * 64;
 typedef __attribute__((ext_vector_type(2))) unsigned int v2u32_t;
 
-template <bool GELU>
+// RAG: W % PX != 0 (a ragged last strip per row; the stride-2 form drops the per-pixel
+// range selects when every strip is whole, as at all TinyViT widths)
+template <bool GELU, bool RAG>
 __global__ __launch_bounds__(256, 2) void dwb_kernel(const __bf16* dy, const __bf16* x, ChanAffine bn,
                                                      const float* w, __bf16* dz, float* part_w, float* part_bn,
                                                      int H, int W, int C, int remap) {
@@ -933,7 +935,7 @@ __global__ __launch_bounds__(256, 2) void dwb_kernel(const __bf16* dy, const __b
       const uint32_t off0 = (uint32_t)((yi * W + xi0) * C + c0) * 2u;
       uint32_t offp[PX];
 #pragma unroll
-      for (int p = 0; p < PX; ++p) offp[p] = xi0 + p < W ? off0 + (uint32_t)(p * C * 2) : 0x80000000u;
+      for (int p = 0; p < PX; ++p) offp[p] = (!RAG || xi0 + p < W) ? off0 + (uint32_t)(p * C * 2) : 0x80000000u;
       float h[PX][4], gg[PX][4], g[PX][4];
       bf16x4 xs[PX];                     // x itself (xhat is formed after the tap loop)
       {
@@ -945,7 +947,7 @@ __global__ __launch_bounds__(256, 2) void dwb_kernel(const __bf16* dy, const __b
           xs[p] = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(xr, offp[p], 0, 0));
 #pragma unroll
         for (int p = 0; p < PX; ++p) {
-          const bool ok = xi0 + p < W;
+          const bool ok = !RAG || xi0 + p < W;
 #pragma unroll
           for (int j = 0; j < 4; j += 2) {   // packed pairs (gelu_phi_pair_t)
             const f32x2 u = vfma(f32x2{(float)xs[p][j], (float)xs[p][j + 1]}, f32x2{sc[j], sc[j + 1]},
@@ -1042,7 +1044,7 @@ __global__ __launch_bounds__(256, 2) void dwb_kernel(const __bf16* dy, const __b
 // once, x twice, dz written and read once, GELU evaluated once per element.
 constexpr int DWB2_PX = 4, DWB2_TYO = 2, DWB2_PAD = 2 * 64;
 
-template <bool GELU>
+template <bool GELU, bool RAG>
 __global__ __launch_bounds__(256, 2) void dwb2_kernel(const __bf16* dy, const __bf16* x, ChanAffine bn,
                                                       const float* w, __bf16* dz, float* part_w, float* part_bn,
                                                       int H, int W, int C, int Ho, int Wo, int remap) {
@@ -1109,7 +1111,7 @@ __global__ __launch_bounds__(256, 2) void dwb2_kernel(const __bf16* dy, const __
       const uint32_t off0 = (uint32_t)((yi * W + xi0) * C + c0) * 2u;
       uint32_t offp[PX];
 #pragma unroll
-      for (int p = 0; p < PX; ++p) offp[p] = xi0 + p < W ? off0 + (uint32_t)(p * C * 2) : 0x80000000u;
+      for (int p = 0; p < PX; ++p) offp[p] = (!RAG || xi0 + p < W) ? off0 + (uint32_t)(p * C * 2) : 0x80000000u;
       float h[PX][4], gg[PX][4], g[PX][4];
       bf16x4 xs[PX];
       {
@@ -1121,7 +1123,7 @@ __global__ __launch_bounds__(256, 2) void dwb2_kernel(const __bf16* dy, const __
           xs[p] = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(xr, offp[p], 0, 0));
 #pragma unroll
         for (int p = 0; p < PX; ++p) {
-          const bool ok = xi0 + p < W;
+          const bool ok = !RAG || xi0 + p < W;
 #pragma unroll
           for (int j = 0; j < 4; j += 2) {   // packed pairs (gelu_phi_pair_t)
             const f32x2 u = vfma(f32x2{(float)xs[p][j], (float)xs[p][j + 1]}, f32x2{sc[j], sc[j + 1]},
@@ -1231,7 +1233,30 @@ __global__ __launch_bounds__(256) void dwb_dx_kernel(const __bf16* x, ChanAffine
   }
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = min(M, r0 + rows_per_block);
-  for (int64_t row = r0 + r; row < r1; row += rpp) {
+  // four rows per step, all loads issued before the first store: dz is rewritten in place,
+  // so the compiler cannot hoist the next row's loads above this row's store by itself
+  // (one 32-B load pair in flight per lane streamed at ~4.4 TB/s)
+  constexpr int U = 4;
+  int64_t row = r0 + r;
+  for (; row + (U - 1) * rpp < r1; row += U * rpp) {
+    uint4 xr[U], dr[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t e = (row + u * rpp) * C + chunk * 8;
+      xr[u] = *(const uint4*)(x + e);
+      dr[u] = *(const uint4*)(dz + e);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float xv[8], dv[8], o[8];
+      load8((const __bf16*)&xr[u], xv);
+      load8((const __bf16*)&dr[u], dv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = wr[j] * (dv[j] - k0[j] - (xv[j] - mu[j]) * rs[j] * k1[j]);
+      store8(dz + (row + u * rpp) * C + chunk * 8, o);
+    }
+  }
+  for (; row < r1; row += rpp) {
     const int64_t e = row * C + chunk * 8;
     float xv[8], dv[8], o[8];
     load8(x + e, xv);
@@ -1869,18 +1894,25 @@ static int dwconv_bn_bwd(int stride, int F, int H, int W, int C, const void* dy,
   ChanAffine bn{bn_mean, bn_rstd, bn_w, bn_b, bn_gelu};
   const dim3 grid((C / DWF_CB) * F);
   if (stride == 2) {
-    if (bn_gelu)
-      hipLaunchKernelGGL(dwb2_kernel<true>, grid, dim3(256), lds, st, (const __bf16*)dy, (const __bf16*)x, bn, w,
-                         (__bf16*)dx, part_w, part_bn, H, W, C, Ho, Wo, dwf_remap());
+    const bool rag = W % DWB2_PX != 0;
+    if (bn_gelu && !rag)
+      hipLaunchKernelGGL((dwb2_kernel<true, false>), grid, dim3(256), lds, st, (const __bf16*)dy, (const __bf16*)x, bn,
+                         w, (__bf16*)dx, part_w, part_bn, H, W, C, Ho, Wo, dwf_remap());
+    else if (bn_gelu)
+      hipLaunchKernelGGL((dwb2_kernel<true, true>), grid, dim3(256), lds, st, (const __bf16*)dy, (const __bf16*)x, bn,
+                         w, (__bf16*)dx, part_w, part_bn, H, W, C, Ho, Wo, dwf_remap());
     else
-      hipLaunchKernelGGL(dwb2_kernel<false>, grid, dim3(256), lds, st, (const __bf16*)dy, (const __bf16*)x, bn, w,
-                         (__bf16*)dx, part_w, part_bn, H, W, C, Ho, Wo, dwf_remap());
-  } else if (bn_gelu) {
-    hipLaunchKernelGGL(dwb_kernel<true>, grid, dim3(256), lds, st, (const __bf16*)dy, (const __bf16*)x, bn, w,
-                       (__bf16*)dx, part_w, part_bn, H, W, C, dwf_remap());
+      hipLaunchKernelGGL((dwb2_kernel<false, true>), grid, dim3(256), lds, st, (const __bf16*)dy, (const __bf16*)x, bn,
+                         w, (__bf16*)dx, part_w, part_bn, H, W, C, Ho, Wo, dwf_remap());
   } else {
-    hipLaunchKernelGGL(dwb_kernel<false>, grid, dim3(256), lds, st, (const __bf16*)dy, (const __bf16*)x, bn, w,
-                       (__bf16*)dx, part_w, part_bn, H, W, C, dwf_remap());
+    // (the range-select-free stride-1 form measured 256 VGPRs + 304 B of scratch: the
+    // compiler's schedule of the select-free GELU chains; it keeps the ragged form)
+    if (bn_gelu)
+      hipLaunchKernelGGL((dwb_kernel<true, true>), grid, dim3(256), lds, st, (const __bf16*)dy, (const __bf16*)x, bn,
+                         w, (__bf16*)dx, part_w, part_bn, H, W, C, dwf_remap());
+    else
+      hipLaunchKernelGGL((dwb_kernel<false, true>), grid, dim3(256), lds, st, (const __bf16*)dy, (const __bf16*)x, bn,
+                         w, (__bf16*)dx, part_w, part_bn, H, W, C, dwf_remap());
   }
   colred(part_w, F, C * 9, nullptr, dw, 1, st);
   colred(part_bn, F, 2 * C, sums, nullptr, 0, st);

@@ -525,11 +525,10 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const TD* dy, const TI* 
   }
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = min(M, r0 + rows_per_block);
-  for (int64_t row = r0 + cm.r; row < r1; row += cm.rpp) {
+  // two rows per step with both rows' inputs loaded first (dx may alias dy)
+  auto one = [&](int64_t row, const float (&xv)[8], const float (&dv)[8]) {
     const int64_t e = row * ld + cm.chunk * 8;
-    float xv[8], dv[8], o[8];
-    load8(x + e, xv);
-    load8(dy + e, dv);
+    float o[8];
     const float rsc = row_scale ? row_scale[row / rpg] : 1.f;
 #pragma unroll
     for (int j = 0; j < 8; j += 2) {   // packed pairs (gelu_phi_pair_t)
@@ -540,6 +539,24 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const TD* dy, const TI* 
       for (int i = 0; i < 2; ++i) o[j + i] = ww[j + i] * rs[j + i] * (gg[i] - k0[j + i] - xh[i] * k1[j + i]);
     }
     store8(dx + e, o);
+  };
+  int64_t row = r0 + cm.r;
+  for (; row + cm.rpp < r1; row += 2 * cm.rpp) {
+    const int64_t e0 = row * ld + cm.chunk * 8, e1 = e0 + (int64_t)cm.rpp * ld;
+    float x0[8], d0[8], x1[8], d1[8];
+    load8(x + e0, x0);
+    load8(dy + e0, d0);
+    load8(x + e1, x1);
+    load8(dy + e1, d1);
+    one(row, x0, d0);
+    one(row + cm.rpp, x1, d1);
+  }
+  if (row < r1) {
+    const int64_t e0 = row * ld + cm.chunk * 8;
+    float x0[8], d0[8];
+    load8(x + e0, x0);
+    load8(dy + e0, d0);
+    one(row, x0, d0);
   }
 }
 
