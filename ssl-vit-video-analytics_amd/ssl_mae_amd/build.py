@@ -22,11 +22,27 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", CSRC, "-I
 # Per-source extra flags.  fed.hip reproduces the reference's separately rounded
 # multiply and add bit for bit; hipcc's default -ffp-contract=fast ignores
 # `#pragma clang fp contract`, so contraction is switched off for that file.
-FILE_FLAGS = {"fed.hip": ["-ffp-contract=off"], "attention.hip": ["-fno-slp-vectorize"]}
+FILE_FLAGS = {"fed.hip": ["-ffp-contract=off"], "attention.hip": ["-fno-slp-vectorize"], "gemm.hip": ["-fno-slp-vectorize"]}
 
 
 def _sources():
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+
+
+def _flag_tag(src):
+    import zlib
+    flags = " ".join([HIPCC] + FLAGS + FILE_FLAGS.get(os.path.basename(src), []))
+    return f"{zlib.crc32(flags.encode()):08x}"
+
+
+def needs_build():
+    lib_t = os.path.getmtime(LIB) if os.path.exists(LIB) else -1.0
+    if lib_t < _newest_input():
+        return True
+    # a compile-flag change leaves the sources older than the library: rebuild when any
+    # source's flag-tagged object is missing
+    return any(not os.path.exists(os.path.join(BUILD, f"{os.path.basename(s)}.{_flag_tag(s)}.o"))
+               for s in _sources()) and os.path.isdir(BUILD)
 
 
 def _newest_input():
@@ -34,16 +50,13 @@ def _newest_input():
     return max(os.path.getmtime(f) for f in files)
 
 
-def needs_build():
-    return not os.path.exists(LIB) or os.path.getmtime(LIB) < _newest_input()
-
-
 def build(verbose=False, jobs=None):
     if not needs_build():
         return LIB
     os.makedirs(BUILD, exist_ok=True)
     srcs = _sources()
-    objs = [os.path.join(BUILD, os.path.basename(s) + ".o") for s in srcs]
+    # the object name carries a hash of its compile flags, so a flag change rebuilds it
+    objs = [os.path.join(BUILD, f"{os.path.basename(s)}.{_flag_tag(s)}.o") for s in srcs]
 
     headers = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(INCLUDE, "*.h"))
     hdr_t = max(os.path.getmtime(f) for f in headers) if headers else 0.0
