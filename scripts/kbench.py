@@ -181,6 +181,13 @@ def gemmw(args):
     t = timeit(lambda: out.zero_(), args.iters)
     print(f"fill [M={M}, {N}] bf16: {t:7.3f} ms  {gbw / t:6.2f} TB/s written", flush=True)
     del out
+    # the same bytes written as N = 128 (one n-tile per row: each block writes whole rows)
+    x = torch.randn(3 * M, 8, device="cuda").to(torch.bfloat16)
+    w = torch.randn(128, 8, device="cuda").to(torch.bfloat16)
+    t = timeit(lambda: K.linear(x, w), args.iters)
+    print(f"linear M={3 * M} N=128 K=8: {t:7.3f} ms  {gbw / t:6.2f} TB/s written", flush=True)
+    del x, w
+    torch.cuda.empty_cache()
     for Kd in (8, 32, 96):
         x = torch.randn(M, Kd, device="cuda").to(torch.bfloat16)
         w = torch.randn(N, Kd, device="cuda").to(torch.bfloat16)

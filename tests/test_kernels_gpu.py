@@ -825,13 +825,16 @@ def test_linear_dw_se_operand(Fr, HW, N, C, acc):
 
 
 @pytest.mark.parametrize("M,N,Kd,upd", [(100000, 384, 96, 2), (1000, 384, 96, 1), (100, 96, 64, 1), (4097, 40, 32, 2),
-                                        (12544 * 32, 384, 96, 2)])
+                                        (12544 * 32, 384, 96, 2), (12544 * 32 + 77, 384, 96, 1),
+                                        (12544 * 32, 384, 64, 1)])
 def test_linear_bn_stats(M, N, Kd, upd):
     """Expand conv + its BatchNorm statistics from the GEMM epilogue (sm_linear_bn_stats):
     y bit-identical to linear(), mean / rstd / running statistics within fp32 rounding of
     bn_stats() over the same stored y (different fixed summation order), and
     num_batches_tracked advanced `upd` times.  Shapes: ragged M (partial tiles and 64-row
-    slabs past M), the BM = 128 tile (M < 192), a ragged output width (N = 40)."""
+    slabs past M), the BM = 128 tile (M < 192), a ragged output width (N = 40); M >= 12544 * 32
+    takes the persistent GEMM form (>= 2048 tiles, K <= 128: both linear() and
+    linear_bn_stats()), ragged and with one K-step (K = 64), checked against fp32 torch."""
     kk = KK()
     x = rnd(M, Kd, dtype=torch.bfloat16, seed=200).to(DEV)
     w = rnd(N, Kd, dtype=torch.bfloat16, seed=201, scale=0.3).to(DEV)
@@ -849,6 +852,8 @@ def test_linear_bn_stats(M, N, Kd, upd):
     yf = y1.float()
     assert rel_err(m2, yf.mean(0)) < 1e-4
     assert rel_err(r2, 1.0 / torch.sqrt(yf.var(0, unbiased=False) + 1e-5)) < 1e-4
+    if M >= 100000:
+        assert rel_err(y1, x.float() @ w.float().t()) < TOL[torch.bfloat16]
 
 
 @pytest.mark.parametrize("shape,frames", [((2, 3, 3, 37, 30), False), ((1, 3, 8, 224, 224), False),
