@@ -1,0 +1,8 @@
+# round-end set, part B: rocprof kernel stats of the bench, the per-op ledger
+set -e
+TAG=${1:-r03f}
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 400 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/${TAG}_prof_bench.json 2> gpurun_out/${TAG}_prof_bench.err
+timeout -k 10 300 python scripts/ledger.py --top 80 > gpurun_out/${TAG}_ledger.txt 2> gpurun_out/${TAG}_ledger.err
