@@ -1,0 +1,10 @@
+# attention tests in ab_c/ (HEAD + a candidate patch) and kbench attn A/B: ab_base/ (HEAD) vs ab_c/
+set -e
+TAG=${1:-r03m}
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+(cd ab_c && timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py tests/test_c2_bf16_gpu.py -m gpu -k "attention or attn") > gpurun_out/${TAG}_tests.log 2>&1
+for i in 1 2; do
+(cd ab_base && timeout -k 10 300 python scripts/kbench.py attn --drop 0.1 --iters 5) > gpurun_out/${TAG}_kb_base$i.log 2>&1
+(cd ab_c && timeout -k 10 300 python scripts/kbench.py attn --drop 0.1 --iters 5) > gpurun_out/${TAG}_kb_new$i.log 2>&1
+done
