@@ -35,14 +35,24 @@ def _flag_tag(src):
     return f"{zlib.crc32(flags.encode()):08x}"
 
 
+STAMP = LIB + ".flags"   # the flag tags the library was linked from (one line per source)
+
+
+def _stamp_text():
+    return "".join(f"{os.path.basename(s)} {_flag_tag(s)}\n" for s in _sources())
+
+
 def needs_build():
     lib_t = os.path.getmtime(LIB) if os.path.exists(LIB) else -1.0
     if lib_t < _newest_input():
         return True
-    # a compile-flag change leaves the sources older than the library: rebuild when any
-    # source's flag-tagged object is missing
-    return any(not os.path.exists(os.path.join(BUILD, f"{os.path.basename(s)}.{_flag_tag(s)}.o"))
-               for s in _sources()) and os.path.isdir(BUILD)
+    # a compile-flag change leaves the sources older than the library: rebuild when the
+    # library was linked from objects built with other flags (stamp written at link time;
+    # a library without a stamp is taken as current)
+    if os.path.exists(STAMP):
+        with open(STAMP) as f:
+            return f.read() != _stamp_text()
+    return False
 
 
 def _newest_input():
@@ -82,6 +92,8 @@ def build(verbose=False, jobs=None):
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
     os.replace(tmp, LIB)
+    with open(STAMP, "w") as f:
+        f.write(_stamp_text())
     return LIB
 
 
