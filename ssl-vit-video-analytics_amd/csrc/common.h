@@ -97,7 +97,10 @@ SM_DEV V gelu_phi_pair_t(V x, V* pdf_out) {
   const V e = vexp2((x * x) * V(-0.5f * 1.44269504088896341f));
   const V half_erfc = (p * t) * e;
   if (pdf_out) *pdf_out = e * V(0.39894228040143268f);
-  return vsel_neg(x, half_erfc, V(1.0f) - half_erfc);
+  // 1 - half_erfc as an explicit fma with -1 (exact: one rounding, as the subtraction):
+  // no contraction setting can fuse (p t) e into it differently in the scalar and the
+  // packed form
+  return vsel_neg(x, half_erfc, vfma(half_erfc, V(-1.0f), V(1.0f)));
 }
 template <typename V>
 SM_DEV V gelu_t(V x) {

@@ -47,12 +47,12 @@ def needs_build():
     if lib_t < _newest_input():
         return True
     # a compile-flag change leaves the sources older than the library: rebuild when the
-    # library was linked from objects built with other flags (stamp written at link time;
-    # a library without a stamp is taken as current)
-    if os.path.exists(STAMP):
-        with open(STAMP) as f:
-            return f.read() != _stamp_text()
-    return False
+    # library was linked from objects built with other flags (stamp written at link time).
+    # A library without a stamp cannot show which flags it was built with: stale.
+    if not os.path.exists(STAMP):
+        return True
+    with open(STAMP) as f:
+        return f.read() != _stamp_text()
 
 
 def _newest_input():

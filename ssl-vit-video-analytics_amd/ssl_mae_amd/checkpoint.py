@@ -14,6 +14,10 @@ training-state file next to it with everything needed to continue bit-for-bit:
                AND state/offset, so torch device RNG use after a resume continues the
                stream), numpy / python RNG incl. python's cached gauss_next (drive the
                loader's frame-index choice)
+  rng_ranks    the same record for every data-parallel rank (gathered at save time):
+               each replica seeds its own streams (train_ssl_mae.main), so a resume
+               restores rank r's streams on rank r -- the replicas keep drawing
+               different tube masks and dropout / DropPath masks after a resume
 
 Everything is a tensor / number / string, so `torch.load(..., weights_only=True)`
 reads it back.
@@ -53,16 +57,39 @@ def _set_rng_state(st):
             torch.cuda.set_rng_state_all(st["cuda_states"])   # seed and offset
 
 
-def save_training_state(path, model, optimizer, scaler, epoch):
-    """Write the full resumable state of an MAE run to `path`."""
+def _dist_world():
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def gather_rng_states():
+    """Every rank's RNG record, in rank order (collective when data parallel: call it on
+    all ranks, then let rank 0 write the file)."""
+    st = _rng_state()
+    rank, world = _dist_world()
+    if world == 1:
+        return [st]
+    import torch.distributed as dist
+    out = [None] * world
+    dist.all_gather_object(out, st)
+    return out
+
+
+def save_training_state(path, model, optimizer, scaler, epoch, rng_states=None):
+    """Write the full resumable state of an MAE run to `path`.  `rng_states`: the
+    per-rank records from gather_rng_states() (default: this process only)."""
     path = Path(path)
     path.parent.mkdir(parents=True, exist_ok=True)
+    rng_states = list(rng_states) if rng_states is not None else [_rng_state()]
     state = {"model": {k: v.detach().cpu() for k, v in model.state_dict().items()},
              "optimizer": _to_cpu(optimizer.state_dict()),
              "scaler": scaler.state_dict() if scaler is not None else {},
              "epoch": int(epoch),
              "forward_count": int(getattr(model, "_sm_fwd_count", 0)),
-             "rng": _rng_state()}
+             "rng": rng_states[0],
+             "rng_ranks": rng_states}
     tmp = path.with_suffix(path.suffix + ".tmp")
     torch.save(state, tmp)
     tmp.replace(path)
@@ -81,8 +108,25 @@ def load_training_state(path, model, optimizer, scaler=None):
     if scaler is not None and state.get("scaler"):
         scaler.load_state_dict(state["scaler"])
     model._sm_fwd_count = int(state.get("forward_count", 0))
-    _set_rng_state(state["rng"])
+    restore_rank_rng(state)
     return int(state["epoch"]) + 1
+
+
+def restore_rank_rng(state):
+    """This rank's streams: rng_ranks[rank] when the file was written by a run of the
+    same world size; otherwise rank 0's record, re-seeded on ranks > 0 with the rank
+    mixed in (a file from a single-process run, or another world size), so the
+    replicas still draw independent masks."""
+    rank, world = _dist_world()
+    ranks = state.get("rng_ranks")
+    if ranks is not None and len(ranks) == world:
+        _set_rng_state(ranks[rank])
+        return
+    _set_rng_state(state["rng"])
+    if rank > 0:
+        from .utils import set_seed
+        base = int(torch.randint(0, 2 ** 30, (1,)).item())
+        set_seed(base + 1000 * rank)
 
 
 def _to_cpu(x):

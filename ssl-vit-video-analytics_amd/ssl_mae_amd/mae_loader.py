@@ -20,10 +20,16 @@ the per-sample noise is drawn on the host from torch's global CPU generator exac
 as the reference draws it (B calls of torch.rand(L) == torch.rand(B, L)); the
 ranking, the [B,T,L] expansion and the row-major compaction of masked token
 indices run in one HIP kernel (sm_tube_mask).  The result is a bool tensor on the
-GPU (the reference's `.to(device)` is then a no-op).  Ties in the noise are broken
-by lower index first; the reference's torch CPU argsort is not stable for L > 16,
-so a tie that straddles the int(r*L) cut (probability ~2e-5 per sample at L=784)
-may resolve differently — see DESIGN.md.
+GPU (the reference's `.to(device)` is then a no-op).  The kernel breaks ties in the
+noise by lower index first, while the reference takes torch's CPU
+`argsort(descending=True)`, which is not stable for L > 16.  The two can differ only
+where equal noise values straddle the int(r*L) cut (~2e-5 per sample at L=784), and
+the host removes exactly that case before the copy (`resolve_cut_ties`): one row sort
+of the batch's noise in numpy (~0.5 ms at B=256, L=784) finds the samples whose
+n_mask-th and (n_mask+1)-th largest values are equal, and for those samples only the
+noise row is replaced by distinct values in the order of the reference's own
+`torch.argsort(noise[b], descending=True)`.  The kernel's ranking then reproduces the
+reference's selection by construction.
 """
 import os
 
@@ -116,12 +122,38 @@ class ClipNormalizer:
         return K.frames_normalize(f.contiguous(), self.mean, self.std, self.bgr_swap, v)
 
 
+def resolve_cut_ties(noise, num_mask):
+    """noise [B, L] fp32 (CPU): rows where equal values straddle the num_mask cut are
+    replaced in place by distinct values ranked as the reference's
+    torch.argsort(noise[b], descending=True) (mae_loader.py:86) ranks them; every other
+    row is left untouched (the lower-index tie rule of sm_tube_mask cannot change
+    which positions are selected there).  Returns the list of replaced rows."""
+    B, L = noise.shape
+    if num_mask <= 0 or num_mask >= L:
+        return []
+    s = np.sort(noise.numpy(), axis=1)
+    rows = np.nonzero(s[:, L - num_mask] == s[:, L - num_mask - 1])[0].tolist()
+    for b in rows:
+        perm = torch.argsort(noise[b], descending=True)
+        ranked = torch.empty(L, dtype=noise.dtype)
+        ranked[perm] = torch.arange(L, 0, -1, dtype=noise.dtype)   # rank 0 -> largest
+        noise[b] = ranked
+    return rows
+
+
+def tube_mask_from_noise(noise, num_frames, num_mask, device="cuda"):
+    """noise [B, L] fp32 on the host -> (bool mask [B,T,L], int32 row-major index list) on
+    `device`, selecting exactly the reference's argsort(descending)[:num_mask] per row."""
+    noise = noise.clone()
+    resolve_cut_ties(noise, num_mask)
+    m8, idx = K.tube_mask(noise.to(device, non_blocking=True), num_frames, num_mask)
+    return m8.view(torch.bool), idx
+
+
 def tube_mask_with_index(batch_size, num_frames, num_patches, mask_ratio, device="cuda"):
     num_mask = int(mask_ratio * num_patches)
     noise = torch.rand(batch_size, num_patches)          # global CPU generator, reference order
-    noise = noise.to(device, non_blocking=True)
-    m8, idx = K.tube_mask(noise, num_frames, num_mask)
-    return m8.view(torch.bool), idx
+    return tube_mask_from_noise(noise, num_frames, num_mask, device)
 
 
 def get_tube_mask(batch_size, num_frames, num_patches, mask_ratio, device="cuda"):

@@ -35,7 +35,7 @@ import torch.distributed as dist
 from . import dist as smdist
 from . import ops as K    # every kernel launch through the torch.ops.ssl_mae dispatcher
 from .functions import mae_loss, masked_pred_std
-from .checkpoint import load_training_state, save_training_state
+from .checkpoint import gather_rng_states, load_training_state, save_training_state
 from .mae_loader import ClipNormalizer, LazyVideoMAEDataset, collate_frames, tube_mask_with_index
 from .mae_vit_adapter import TinyVideoMAE
 from .optim import FusedAdamW, GradScaler
@@ -232,10 +232,11 @@ def main(argv=None):
         logger.info(f"    Total Training ETA: {format_time(eta)}")
         logger.info("-" * 30)
         if epoch % 10 == 0:
+            rngs = gather_rng_states()            # every replica's streams (collective)
             if rank == 0:
                 p = save_dir / f"encoder_ep{epoch}.pth"
                 save_checkpoint(model.encoder.state_dict(), p)
-                save_training_state(save_dir / "last_state.pth", model, optimizer, scaler, epoch)
+                save_training_state(save_dir / "last_state.pth", model, optimizer, scaler, epoch, rngs)
                 logger.info(f"Checkpoint saved to {p}")
             if world > 1:
                 dist.barrier()

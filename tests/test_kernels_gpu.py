@@ -537,6 +537,22 @@ def test_tube_mask_and_gather_bit_exact():
     assert abs(sd.item() - pred[ref.reshape(-1)].float().std().item()) < 1e-4
 
 
+def test_tube_mask_constructed_cut_ties():
+    """Equal noise values straddling the int(r*L) cut: the host tie resolution +
+    sm_tube_mask select exactly the reference's argsort(descending)[:n] (mae_loader.py:86)
+    and emit the row-major index list of that mask."""
+    from test_tube_mask_cpu import constructed_cut_ties, reference_select
+    from ssl_mae_amd.mae_loader import tube_mask_from_noise
+    B, T, L, nm = 32, 8, 784, 588
+    noise = constructed_cut_ties(B, L, nm, seed=11)
+    noise[5] = torch.rand(L)                 # a row with no tie at the cut
+    mask, idx = tube_mask_from_noise(noise, T, nm, DEV)
+    ref = torch.stack([torch.from_numpy(reference_select(noise[b], nm)) for b in range(B)])
+    ref = ref[:, None, :].expand(B, T, L).contiguous()
+    assert torch.equal(mask.cpu(), ref)
+    assert torch.equal(idx.cpu(), torch.nonzero(ref.reshape(-1)).reshape(-1).int())
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_mae_loss(dtype):
     from oracle import mae_oracle as O
