@@ -85,6 +85,29 @@ int sm_linear_se(int rows, int nout, int nin, const void* a2, const void* w, con
  * [rows][nin] bf16, gate [rows / hw][nin] fp32 (the SE sigmoid), dy [rows][nout] bf16,
  * fp32 dW.  h3 is formed in the GEMM's operand loads exactly as sm_se_scale stores it:
  * bit-identical to sm_se_scale + sm_gemm.  hw % 64 == 0. */
+/* ---- the stem's BN2 folded into stage 0's first MBConv (tiny_vit.py:62-72 feeding :43;
+ * replaces the aten batch_norm output the reference materialises between PatchEmbed and
+ * stages[0][0]): y = x W^T with x = bf16(a sc + sh), sc = a_rstd a_w, sh = a_b - a_mean sc,
+ * formed in the A-operand loads exactly as sm_bn_apply stores x (bit-identical to
+ * sm_bn_apply + sm_gemm / sm_linear_bn_stats).  a [M][K] bf16, K % 8 == 0, K <= 256, w [N][K]
+ * bf16, y [M][N] bf16.  _bn_stats: plus the output's train-mode BatchNorm statistics
+ * (workspace sm_linear_bn_stats_workspace_bytes). */
+int sm_linear_bnin(int M, int N, int K, const void* a, const float* a_mean, const float* a_rstd,
+                   const float* a_w, const float* a_b, const void* w, void* y, hipStream_t stream);
+int sm_linear_bnin_bn_stats(int M, int N, int K, const void* a, const float* a_mean, const float* a_rstd,
+                            const float* a_w, const float* a_b, const void* w, void* y, float* mean,
+                            float* rstd, float* run_mean, float* run_var, int64_t* num_batches_tracked,
+                            float momentum, float eps, int updates, void* ws, int64_t ws_bytes,
+                            hipStream_t stream);
+/* sm_bn_apply whose residual R is stored before its own BatchNorm (r_*): R's value is the
+ * BN output bf16(R r_sc + r_sh) exactly as sm_bn_apply stores it (the MBConv residual of
+ * stages[0][0] over the stem's BN2, tiny_vit.py:54-56). */
+int sm_bn_apply_res_bn(int x_dtype, int y_dtype, int64_t M, int C, const void* x, const float* mean,
+                       const float* rstd, const float* w, const float* b, void* y, int gelu, const void* R,
+                       const float* r_mean, const float* r_rstd, const float* r_w, const float* r_b,
+                       const float* row_scale, int64_t rows_per_group, hipStream_t st);
+/* sm_linear_dw_se with gate == NULL: the B operand is the BatchNorm output act(a2) (act_gelu
+ * 0: x = bf16(a2 sc + sh)); rows need not be a multiple of hw. */
 int64_t sm_linear_dw_se_workspace_bytes(int rows, int nout, int nin);
 int sm_linear_dw_se(int rows, int nout, int nin, const void* dy, const void* a2, const float* act_mean,
                     const float* act_rstd, const float* act_w, const float* act_b, int act_gelu, const float* gate,

@@ -3,7 +3,12 @@ import csv
 import sys
 d = sys.argv[1]
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 30
-rows = list(csv.DictReader(open(f"{d}/run_kernel_stats.csv")))
+import glob
+import os
+f = os.path.join(d, "run_kernel_stats.csv")
+if not os.path.exists(f):
+    f = sorted(glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True))[0]
+rows = list(csv.DictReader(open(f)))
 tot = sum(float(r['TotalDurationNs']) for r in rows)
 print(f"total kernel time {tot/1e6:.1f} ms")
 for r in rows[:n]:

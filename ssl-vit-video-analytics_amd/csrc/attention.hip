@@ -178,16 +178,17 @@ SM_DEV uint32_t quad_transpose_bytes(uint32_t v, uint32_t sel1, uint32_t sel2) {
 // LDS stores after the barrier.  The tile's descriptor (scalar) carries the base
 // and num_records = valid rows x row bytes, so rows past L read as zero with no
 // per-lane address arithmetic, compare or branch in the tile loop.
-template <int D, int ROWS>
+template <int D, int ROWS, int NT = 256>
 struct Stager {
-  static constexpr int CH = ROWS * D / 8 / 256;
+  static constexpr int CH = ROWS * D / 8 / NT;
+  static_assert(CH >= 1 && CH * NT * 8 == ROWS * D, "tile must split evenly over the block's threads");
   uint32_t voff[CH];
   int loff[CH], ld;
   SM_DEV void init(int ld_) {
     ld = ld_;
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
-      const int c = threadIdx.x + 256 * i;
+      const int c = threadIdx.x + NT * i;
       const int row = c / (D / 8), d = (c % (D / 8)) * 8;
       voff[i] = (uint32_t)(row * ld + d) * 2u;
       loff[i] = tile_off<D>(row, d);
@@ -448,15 +449,16 @@ __global__ void attn_delta_kernel(AttnArgs a, int D) {
 // Row constants folded in: without dropout the dP accumulator starts at -Delta
 // (dS = P * acc); with it, log2(1/(1-p)) is folded into the LSE so the exp yields
 // P' = P/(1-p) directly (dV needs no final scale) and Delta is stored as Delta(1-p).
-template <int D, bool DROP>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(AttnArgs a) {
+template <int D, bool DROP, int NW = 4, bool PRIO = false>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_bf16(AttnArgs a) {
   constexpr int QT = 64;
   constexpr int RB = 32 * D * 2;
+  constexpr int KB = 32 * NW;   // keys per block
   __shared__ __attribute__((aligned(16))) char lq[QT * D * 2];
   __shared__ __attribute__((aligned(16))) char ldo[QT * D * 2];
   __shared__ __attribute__((aligned(16))) float llse[QT];
   __shared__ __attribute__((aligned(16))) float ldel[QT];
-  const AttnTile tl((a.L + 127) / 128, a.H);
+  const AttnTile tl((a.L + KB - 1) / KB, a.H);
   const int n = tl.n, hd = tl.hd;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5;
   const int C = a.H * D;
@@ -468,8 +470,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(AttnArgs a) {
   const __bf16* dob = (const __bf16*)a.dout + (int64_t)n * a.L * C + hd * D;
   const float* lse = a.lse + ((int64_t)n * a.H + hd) * a.L;
   const float* del = a.delta + ((int64_t)n * a.H + hd) * a.L;
-  const int key = tl.qb * 128 + w * 32 + (l & 31);
-  const bool wact = tl.qb * 128 + w * 32 < a.L;   // else: only stages tiles (see the forward)
+  const int key = tl.qb * KB + w * 32 + (l & 31);
+  const bool wact = tl.qb * KB + w * 32 < a.L;   // else: only stages tiles (see the forward)
 
   bf16x8 kf[D / 16], vf[D / 16];
 #pragma unroll
@@ -489,7 +491,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(AttnArgs a) {
   for (int s = 0; s < D / 16; ++s)
 #pragma unroll
     for (int j = 0; j < 8; ++j) kf[s][j] = (__bf16)((float)kf[s][j] * (a.scale * LOG2E));
-  Stager<D, QT> sq, sd;
+  Stager<D, QT, 64 * NW> sq, sd;
   sq.init(ldq);
   sd.init(C);
   int roff[D / 16], tlo[D / 32], thi[D / 32];
@@ -576,22 +578,38 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(AttnArgs a) {
       }
   };
 
-  uint4 rq[Stager<D, QT>::CH], rd[Stager<D, QT>::CH];
+  uint4 rq[Stager<D, QT, 64 * NW>::CH], rd[Stager<D, QT, 64 * NW>::CH];
+  // static priority for one wave of each SIMD pair (MI355X_MICROARCH.md item 4): the
+  // younger half of an 8-wave block, or every other 4-wave block
+  if (PRIO && (NW == 8 ? w >= 4 : ((blockIdx.x >> 3) & 1))) __builtin_amdgcn_s_setprio(1);
+  // the tile's row constants (LSE, Delta) are prefetched with its Q / dO rows (wave 0,
+  // one row per lane, index clamped: no branch); loading them between the two barriers
+  // held every wave of the block for a global-load round trip per tile
+  float rlse = 0.f, rdel = 0.f;
+  auto rowc_load = [&](int q0) {
+    if (threadIdx.x < QT) {
+      const int qq = min(q0 + (int)threadIdx.x, a.L - 1);
+      rlse = lse[qq];
+      rdel = del[qq];
+    }
+  };
   sq.load(qb, a.L, rq);
   sd.load(dob, a.L, rd);
+  rowc_load(0);
   for (int q0 = 0; q0 < a.L; q0 += QT) {
     __syncthreads();
     sq.store(lq, rq);
     sd.store(ldo, rd);
     if (threadIdx.x < QT) {
-      const int qq = q0 + threadIdx.x;
-      llse[threadIdx.x] = qq < a.L ? -fmaf(lse[qq], LOG2E, lkeep) : -1e30f;   // negated; invalid rows -> P = 0
-      ldel[threadIdx.x] = qq < a.L ? del[qq] * dkeep : 0.f;
+      const bool ok = q0 + (int)threadIdx.x < a.L;
+      llse[threadIdx.x] = ok ? -fmaf(rlse, LOG2E, lkeep) : -1e30f;   // negated; invalid rows -> P = 0
+      ldel[threadIdx.x] = ok ? rdel * dkeep : 0.f;
     }
     __syncthreads();
     if (q0 + QT < a.L) {
       sq.load(qb + (int64_t)(q0 + QT) * ldq, a.L - q0 - QT, rq);
       sd.load(dob + (int64_t)(q0 + QT) * C, a.L - q0 - QT, rd);
+      rowc_load(q0 + QT);
     }
     if (!wact) continue;
     f32x16 s0, p0, s1, p1;
@@ -620,13 +638,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(AttnArgs a) {
 
 // =============================================================== bf16 backward dQ
 // Queries on lanes; K / V tiles staged with prefetch; dQ^T = K^T dS^T.
-template <int D, bool DROP>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16(AttnArgs a) {
+template <int D, bool DROP, int NW = 4, bool PRIO = false>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_bf16(AttnArgs a) {
   constexpr int KT = 64;
   constexpr int RB = 32 * D * 2;
+  constexpr int QB = 32 * NW;   // queries per block
   __shared__ __attribute__((aligned(16))) char lk[KT * D * 2];
   __shared__ __attribute__((aligned(16))) char lv[KT * D * 2];
-  const AttnTile tl((a.L + 127) / 128, a.H);
+  const AttnTile tl((a.L + QB - 1) / QB, a.H);
   const int n = tl.n, hd = tl.hd;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5;
   const int C = a.H * D;
@@ -636,9 +655,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16(AttnArgs a) {
   const __bf16* kb = qkv + C + hd * D;
   const __bf16* vb = qkv + 2 * C + hd * D;
   const __bf16* dob = (const __bf16*)a.dout + (int64_t)n * a.L * C + hd * D;
-  const int q = tl.qb * 128 + w * 32 + (l & 31);
+  const int q = tl.qb * QB + w * 32 + (l & 31);
   const bool qok = q < a.L;
-  const bool wact = tl.qb * 128 + w * 32 < a.L;   // else: only stages tiles (see the forward)
+  const bool wact = tl.qb * QB + w * 32 < a.L;   // else: only stages tiles (see the forward)
   const float lse2 = qok ? a.lse[((int64_t)n * a.H + hd) * a.L + q] * LOG2E : 1e30f;
 
   // This lane's half of dO's and O's row for query q (D/2 values): Delta = rowsum(dO*O)
@@ -667,7 +686,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16(AttnArgs a) {
   for (int s = 0; s < D / 16; ++s)
 #pragma unroll
     for (int j = 0; j < 8; ++j) qf[s][j] = (__bf16)((float)qf[s][j] * (a.scale * LOG2E));
-  Stager<D, KT> stg;
+  Stager<D, KT, 64 * NW> stg;
   stg.init(ldq);
   int roff[D / 16], tlo[D / 32], thi[D / 32];
 #pragma unroll
@@ -683,9 +702,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16(AttnArgs a) {
   const uint32_t dlb = seed32(a.seed) + (uint32_t)((uint64_t)(n * a.H + hd) * a.L + q) * AG + (uint32_t)h * AC;
   const uint32_t dthr = attn_thr(a.drop_p);
 
-  uint4 rk[Stager<D, KT>::CH], rv[Stager<D, KT>::CH];
+  uint4 rk[Stager<D, KT, 64 * NW>::CH], rv[Stager<D, KT, 64 * NW>::CH];
   stg.load(kb, a.L, rk);
   stg.load(vb, a.L, rv);
+  // static priority for one wave of each SIMD pair (MI355X_MICROARCH.md item 4): the
+  // younger half of an 8-wave block, or every other 4-wave block
+  if (PRIO && (NW == 8 ? w >= 4 : ((blockIdx.x >> 3) & 1))) __builtin_amdgcn_s_setprio(1);
   // one key tile; the ragged last tile is its own instantiation (see the forward)
   auto tile = [&](int k0, auto rag) {
     constexpr bool RAGGED = decltype(rag)::value;
@@ -889,6 +911,33 @@ __global__ __launch_bounds__(128) void attn_bwd_dkdv_f32(AttnArgs a) {
   }
 }
 
+// dQ first: it forms Delta = rowsum(dO*O) in its prologue for the dK/dV kernel
+template <int D, bool DROP>
+void launch_attn_bwd(const AttnArgs& a, int var, hipStream_t st) {
+  const unsigned nh = (unsigned)(a.H * a.N);
+  const dim3 g4((unsigned)((a.L + 127) / 128) * nh), g8((unsigned)((a.L + 255) / 256) * nh);
+  if constexpr (D == 64) {
+    if (var == 1 || var == 2) {
+      hipLaunchKernelGGL((attn_bwd_dq_bf16<D, DROP>), g4, dim3(256), 0, st, a);
+      if (var == 1) hipLaunchKernelGGL((attn_bwd_dkdv_bf16<D, DROP, 8>), g8, dim3(512), 0, st, a);
+      else hipLaunchKernelGGL((attn_bwd_dkdv_bf16<D, DROP, 8, true>), g8, dim3(512), 0, st, a);
+      return;
+    }
+    if (var == 3) {
+      hipLaunchKernelGGL((attn_bwd_dq_bf16<D, DROP, 4, true>), g4, dim3(256), 0, st, a);
+      hipLaunchKernelGGL((attn_bwd_dkdv_bf16<D, DROP, 4, true>), g4, dim3(256), 0, st, a);
+      return;
+    }
+    if (var == 4) {
+      hipLaunchKernelGGL((attn_bwd_dq_bf16<D, DROP, 8, true>), g8, dim3(512), 0, st, a);
+      hipLaunchKernelGGL((attn_bwd_dkdv_bf16<D, DROP, 8, true>), g8, dim3(512), 0, st, a);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((attn_bwd_dq_bf16<D, DROP>), g4, dim3(256), 0, st, a);
+  hipLaunchKernelGGL((attn_bwd_dkdv_bf16<D, DROP>), g4, dim3(256), 0, st, a);
+}
+
 }  // namespace
 
 extern "C" int sm_attn_fwd(int dtype, int N, int L, int H, int D, const void* qkv, void* out,
@@ -926,16 +975,12 @@ extern "C" int sm_attn_bwd(int dtype, int N, int L, int H, int D, const void* qk
   a.qkv = qkv; a.o = o; a.dout = dout; a.lse = (float*)lse; a.delta = delta_ws; a.out = dqkv;
   a.N = N; a.L = L; a.H = H; a.scale = scale; a.drop_p = drop_p; a.seed = seed;
   dim3 grid((L + 127) / 128, H, N);
-  const dim3 grid1((unsigned)(((L + 127) / 128) * H * N));   // bf16 kernels: 1-D, XCD-remapped
   const bool drop = drop_p > 0.f;
   if (dtype == SM_BF16) {
     // dQ first: it forms Delta = rowsum(dO*O) in its prologue for the dK/dV kernel
-#define SM_ATTN_BWD(DD, DR)                                                        \
-  hipLaunchKernelGGL((attn_bwd_dq_bf16<DD, DR>), grid1, dim3(256), 0, st, a);      \
-  hipLaunchKernelGGL((attn_bwd_dkdv_bf16<DD, DR>), grid1, dim3(256), 0, st, a);
-    if (D == 32) { if (drop) { SM_ATTN_BWD(32, true) } else { SM_ATTN_BWD(32, false) } }
-    else { if (drop) { SM_ATTN_BWD(64, true) } else { SM_ATTN_BWD(64, false) } }
-#undef SM_ATTN_BWD
+    static const int var = [] { const char* e = getenv("SM_ATTN_BWD_VAR"); return e ? atoi(e) : 0; }();
+    if (D == 32) { if (drop) launch_attn_bwd<32, true>(a, var, st); else launch_attn_bwd<32, false>(a, var, st); }
+    else { if (drop) launch_attn_bwd<64, true>(a, var, st); else launch_attn_bwd<64, false>(a, var, st); }
   } else {
     const int dblocks = (int)(((int64_t)N * L + 3) / 4);
     hipLaunchKernelGGL(attn_delta_kernel<float>, dim3(dblocks), dim3(256), 0, st, a, D);

@@ -120,6 +120,10 @@ SM_DEV float gelu_grad(float x) { return gelu_grad_t<float>(x); }
 SM_DEV f32x2 gelu_f2(f32x2 x) { return gelu_t<f32x2>(x); }
 SM_DEV f32x2 gelu_grad2(f32x2 x) { return gelu_grad_t<f32x2>(x); }
 
+// BatchNorm shift b - mean * sc as one explicit fma: every kernel that forms the affine
+// (bn_apply and each folded consumer) computes the same bits whatever the contraction mode
+SM_DEV float bn_shift(float b, float mean, float sc) { return fmaf(-mean, sc, b); }
+
 // Per-channel input transform folded into a consumer's loads: h = act(x * sc + sh)
 // with sc = rstd * w, sh = b - mean * sc (train-mode BatchNorm) and act = GELU or
 // identity; rounded to the storage type exactly as bn_apply would store h.  A null
@@ -138,7 +142,7 @@ struct Affine8 {
     for (int j = 0; j < 8; ++j) {
       if (on) {
         sc[j] = a.rstd[c0 + j] * a.w[c0 + j];
-        sh[j] = a.b[c0 + j] - a.mean[c0 + j] * sc[j];
+        sh[j] = bn_shift(a.b[c0 + j], a.mean[c0 + j], sc[j]);
       } else {
         sc[j] = 1.f;
         sh[j] = 0.f;

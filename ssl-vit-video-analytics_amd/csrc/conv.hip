@@ -202,7 +202,7 @@ __global__ __launch_bounds__(SC2_NT, 1) void stem_conv2_kernel(const __bf16* a1,
   if (t < SC2_CIN) {   // = Affine8::init
     const float sc = act.rstd[t] * act.w[t];
     aff[0][t] = sc;
-    aff[1][t] = act.b[t] - act.mean[t] * sc;
+    aff[1][t] = bn_shift(act.b[t], act.mean[t], sc);
   }
   // zero the ring once: halo columns (x = -1, x >= W) and rows outside the image
   for (int i = t; i < SC2_RING / 16; i += SC2_NT) *(uint4*)(lds + 16 * i) = make_uint4(0, 0, 0, 0);
@@ -896,7 +896,7 @@ __global__ __launch_bounds__(256, 2) void dwb_kernel(const __bf16* dy, const __b
     const int c = cs * DWF_CB + t;
     const float r = bn.rstd[c], scv = r * bn.w[c];
     cl[t] = scv;
-    cl[DWF_CB + t] = bn.b[c] - bn.mean[c] * scv;
+    cl[DWF_CB + t] = bn_shift(bn.b[c], bn.mean[c], scv);
     cl[2 * DWF_CB + t] = bn.mean[c];
     cl[3 * DWF_CB + t] = r;
   }
@@ -1075,7 +1075,7 @@ __global__ __launch_bounds__(256, 2) void dwb2_kernel(const __bf16* dy, const __
     const int c = cs * DWF_CB + t;
     const float r = bn.rstd[c], scv = r * bn.w[c];
     cl[t] = scv;
-    cl[DWF_CB + t] = bn.b[c] - bn.mean[c] * scv;
+    cl[DWF_CB + t] = bn_shift(bn.b[c], bn.mean[c], scv);
     cl[2 * DWF_CB + t] = bn.mean[c];
     cl[3 * DWF_CB + t] = r;
   }
@@ -1505,7 +1505,7 @@ struct BnCh8 {   // per-channel constants of the BatchNorm + GELU on 8 channels
       rs[j] = a.rstd[c];
       mr[j] = a.mean[c] * rs[j];
       sc[j] = rs[j] * a.w[c];
-      sh[j] = a.b[c] - a.mean[c] * sc[j];
+      sh[j] = bn_shift(a.b[c], a.mean[c], sc[j]);
       wr[j] = a.w[c] * rs[j];
     }
   }

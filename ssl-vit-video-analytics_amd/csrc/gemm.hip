@@ -535,6 +535,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
 // SIMD at BM = 256.
 constexpr uint32_t BUF_OOB = 0x40000000u;   // >= num_records: the load returns 0
 constexpr int XA_MAXK = 1536;                // IMP 6: channels of the transformed A operand
+constexpr int XB_MAXK = 256;                 // IMP 11 / 12: channels of the BatchNorm-input A operand
 
 template <int ROWS>
 SM_DEV int mnmaj_off_r(int krow, int col) {   // [64][ROWS] MN-major tile (ROWS*2-B rows)
@@ -767,7 +768,8 @@ struct XformColsB {
     }
     if constexpr (IMP == 7) {
       const int c = n0 + col < g.N ? n0 + col : 0;
-      load8(g.xb_gate + (int64_t)(k0 / g.xb_hw) * g.N + c, gt);
+      if (g.xb_gate) load8(g.xb_gate + (int64_t)(k0 / g.xb_hw) * g.N + c, gt);
+      else for (int j = 0; j < 8; ++j) gt[j] = 1.f;   // no gate: x = bf16(BN(a)), as bn_apply stores it
     }
   }
   SM_DEV void store(char* lds, const GemmArgs& g, int n0, int k0) const {
@@ -814,12 +816,18 @@ template <bool AK, bool BK, typename TC, bool VEC, int BMV, int IMP = 0>
 __global__ __launch_bounds__(BMV * 2, (BMV == 256 && IMP != 5 && IMP != 6 && IMP != 7) ? 4 : 2) void gemm_bf16_v2(GemmArgs g) {
   constexpr int NT = BMV * 2, BNV = 128;
   constexpr bool XB = IMP == 5 || IMP == 7;
+  // A (K-major) formed on load: IMP 6 act(x) * gate (SE output); IMP 11 / 12 a BatchNorm
+  // output x = bf16(a sc + sh) from its stored input a (11: plus the IMP 8 statistics)
+  constexpr bool XA = IMP == 6 || IMP == 11 || IMP == 12;
   constexpr int LDS_MAIN = (BMV + BNV) * BKT * 2, LDS_EPI = (NT / 64) * 8192;   // operand tiles | row stage
   __shared__ __attribute__((aligned(16))) char lds[LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI];
   char* la = lds;
   char* lb = lds + BMV * BKT * 2;
   // IMP 6: per-channel table of the A transform (BN scale, shift, SE gate of the tile's frame)
-  __shared__ __attribute__((aligned(16))) float xtab[IMP == 6 ? 3 * XA_MAXK : 4];
+  // (IMP 11 / 12: scale and shift of at most XB_MAXK channels -- a small table keeps two
+  // 256-row blocks per CU)
+  constexpr int XT = IMP == 6 ? XA_MAXK : XB_MAXK;
+  __shared__ __attribute__((aligned(16))) float xtab[IMP == 6 ? 3 * XA_MAXK : XA ? 2 * XB_MAXK : 4];
   // 1-D grid over (split zs, tile), split-major, with the bijective XCD remap: the
   // n-tiles of one m-tile (sharing the A panel) and, under split-K, all tiles of one
   // split (sharing its token rows of both operands) are dealt to one XCD's L2.
@@ -837,13 +845,13 @@ __global__ __launch_bounds__(BMV * 2, (BMV == 256 && IMP != 5 && IMP != 6 && IMP
   const __bf16* B = (const __bf16*)g.B;
   const int kb = g.k_begin + zs * g.k_chunk;
   const int ke = min(g.K, kb + g.k_chunk);
-  if constexpr (IMP == 6) {   // the tile's rows lie in one frame (host: xb_hw % BMV == 0)
-    const int64_t frame = (int64_t)m0 / g.xb_hw;
+  if constexpr (XA) {   // IMP 6: the tile's rows lie in one frame (host: xb_hw % BMV == 0)
+    const int64_t frame = IMP == 6 ? (int64_t)m0 / g.xb_hw : 0;
     for (int c = threadIdx.x; c < g.K; c += NT) {
       const float sc = g.xb_act.rstd[c] * g.xb_act.w[c];   // = Affine8::init
       xtab[c] = sc;
-      xtab[XA_MAXK + c] = g.xb_act.b[c] - g.xb_act.mean[c] * sc;
-      xtab[2 * XA_MAXK + c] = g.xb_gate[frame * g.K + c];
+      xtab[XT + c] = bn_shift(g.xb_act.b[c], g.xb_act.mean[c], sc);
+      if constexpr (IMP == 6) xtab[2 * XA_MAXK + c] = g.xb_gate[frame * g.K + c];
     }
     __syncthreads();
   }
@@ -907,24 +915,43 @@ __global__ __launch_bounds__(BMV * 2, (BMV == 256 && IMP != 5 && IMP != 6 && IMP
     }
     if constexpr (IMP == 1 || IMP == 10) {
       cla.store(la, ra);
-    } else if constexpr (IMP == 6) {
-      // h3 = bf16(bf16(GELU(a2 sc + sh)) * gate), exactly as se_apply_kernel stores it;
-      // the thread's 8 channels are fixed per K-step (k0 + kk0 ..)
+    } else if constexpr (XA) {
+      // h3 = bf16(bf16(GELU(a2 sc + sh)) * gate), exactly as se_apply_kernel stores it
+      // (no gate: x = bf16(a2 sc + sh), exactly as bn_apply stores it); the thread's 8
+      // channels are fixed per K-step (k0 + kk0 ..)
       const int c0 = k0 + tla.kk0;
-      float sc[8], sh[8], gt[8];
-      load8(xtab + c0, sc);
-      load8(xtab + XA_MAXK + c0, sh);
-      load8(xtab + 2 * XA_MAXK + c0, gt);
+      if constexpr (IMP == 6) {
+        float sc[8], sh[8], gt[8];
+        load8(xtab + c0, sc);
+        load8(xtab + XA_MAXK + c0, sh);
+        load8(xtab + 2 * XA_MAXK + c0, gt);
 #pragma unroll
-      for (int i = 0; i < TileLoader<BMV, NT, AK>::CH; ++i) {
-        float v[8];
-        load8((const __bf16*)&ra[i], v);
+        for (int i = 0; i < TileLoader<BMV, NT, AK>::CH; ++i) {
+          float v[8];
+          load8((const __bf16*)&ra[i], v);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float t = v[j] * sc[j] + sh[j];
-          v[j] = to_f<__bf16>(from_f<__bf16>(g.xb_act.gelu ? gelu_f(t) : t)) * gt[j];
+          for (int j = 0; j < 8; ++j) {
+            const float t = fmaf(v[j], sc[j], sh[j]);
+            v[j] = to_f<__bf16>(from_f<__bf16>(g.xb_act.gelu ? gelu_f(t) : t)) * gt[j];
+          }
+          ra[i] = pack8(v, (__bf16*)nullptr);
         }
-        ra[i] = pack8(v, (__bf16*)nullptr);
+      } else {
+        // x = bf16(a sc + sh), as bn_apply stores it; one channel pair at a time (few live
+        // registers beside the accumulators: the plain kernel's 4 waves / SIMD)
+#pragma unroll
+        for (int jp = 0; jp < 4; ++jp) {
+          const float2 sc2 = *(const float2*)(xtab + c0 + 2 * jp);
+          const float2 sh2 = *(const float2*)(xtab + XT + c0 + 2 * jp);
+#pragma unroll
+          for (int i = 0; i < TileLoader<BMV, NT, AK>::CH; ++i) {
+            uint32_t* wv = (uint32_t*)&ra[i];
+            const float lo = __uint_as_float(wv[jp] << 16), hi = __uint_as_float(wv[jp] & 0xFFFF0000u);
+            typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+            const bf16x2 o = {(__bf16)fmaf(lo, sc2.x, sh2.x), (__bf16)fmaf(hi, sc2.y, sh2.y)};
+            wv[jp] = __builtin_bit_cast(uint32_t, o);
+          }
+        }
       }
       tla.store(la, ra);
     } else {
@@ -967,7 +994,8 @@ __global__ __launch_bounds__(BMV * 2, (BMV == 256 && IMP != 5 && IMP != 6 && IMP
     }
     __syncthreads();
   }
-  gemm_epilogue<TC, VEC, 2, 2, IMP == 8 || IMP == 10, IMP == 9>(g, acc, m0, n0, wm, wn, l, zs, lds + w * 8192);
+  gemm_epilogue<TC, VEC, 2, 2, IMP == 8 || IMP == 10 || IMP == 11, IMP == 9>(g, acc, m0, n0, wm, wn, l, zs,
+                                                                          lds + w * 8192);
 }
 
 // ============================================================ f32 MFMA kernel
@@ -1541,6 +1569,64 @@ extern "C" int sm_conv3x3_fwd_bn_stats(const void* x, const void* wpack, void* y
                                    eps, updates, fin, 2 * (int64_t)Cout * 8, st);
 }
 
+// The stem's BN2 folded into stage 0's first MBConv (tiny_vit.py:62-72 -> :43): the expand
+// conv's A operand is the BatchNorm output x = bf16(a sc + sh) formed from the stored conv
+// output a in the operand loads (IMP 11 / 12; sc = rstd w, sh = b - mean sc, exactly as
+// sm_bn_apply stores x), so x is never written.  _bn_stats: plus the output's BatchNorm
+// statistics (IMP 11, as sm_linear_bn_stats).  a [M][K] bf16, K % 8 == 0, K <= 1536.
+static int linear_bnin_launch(int M, int N, int K, const void* a, const float* mean, const float* rstd,
+                              const float* bw, const float* bb, const void* w, void* y, float* stat_part,
+                              hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (K <= 0 || K % 8 || K > XB_MAXK || N % 8 || mean == nullptr || rstd == nullptr || bw == nullptr ||
+      bb == nullptr || (((uintptr_t)a | (uintptr_t)w | (uintptr_t)y) & 15))
+    return -2;
+  GemmArgs g{};
+  g.M = M; g.N = N; g.K = K; g.A = a; g.lda = K; g.B = w; g.ldb = K; g.C = y; g.ldc = N;
+  g.alpha = 1.f; g.beta = 0.f; g.rows_per_group = 1; g.k_begin = 0; g.k_chunk = K;
+  g.xb_act = ChanAffine{mean, rstd, bw, bb, 0};
+  g.stat_part = stat_part;
+  const int tiles_n = (N + 127) / 128;
+  if (gemm_variant(M, N, K) == 2) {
+    const dim3 grid(tiles_n * ((M + 255) / 256));
+    if (stat_part) hipLaunchKernelGGL((gemm_bf16_v2<true, true, __bf16, true, 256, 11>), grid, dim3(512), 0, stream, g);
+    else hipLaunchKernelGGL((gemm_bf16_v2<true, true, __bf16, true, 256, 12>), grid, dim3(512), 0, stream, g);
+  } else {
+    const dim3 grid(tiles_n * ((M + 127) / 128));
+    if (stat_part) hipLaunchKernelGGL((gemm_bf16_v2<true, true, __bf16, true, 128, 11>), grid, dim3(256), 0, stream, g);
+    else hipLaunchKernelGGL((gemm_bf16_v2<true, true, __bf16, true, 128, 12>), grid, dim3(256), 0, stream, g);
+  }
+  SM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int sm_linear_bnin(int M, int N, int K, const void* a, const float* a_mean, const float* a_rstd,
+                              const float* a_w, const float* a_b, const void* w, void* y, hipStream_t stream) {
+  return linear_bnin_launch(M, N, K, a, a_mean, a_rstd, a_w, a_b, w, y, nullptr, stream);
+}
+
+extern "C" int sm_linear_bnin_bn_stats(int M, int N, int K, const void* a, const float* a_mean, const float* a_rstd,
+                                       const float* a_w, const float* a_b, const void* w, void* y, float* mean,
+                                       float* rstd, float* run_mean, float* run_var, int64_t* num_batches_tracked,
+                                       float momentum, float eps, int updates, void* ws, int64_t ws_bytes,
+                                       hipStream_t stream) {
+  if (M <= 0 || N <= 0) return -2;
+  if (ws_bytes < sm_linear_bn_stats_workspace_bytes(M, N)) return -4;
+  const int64_t nparts = (M + 63) / 64;
+  float* part = (float*)ws;
+  float* part2 = part + nparts * 2 * N;
+  void* fin = (void*)(((uintptr_t)(part2 + (int64_t)LBS_CHUNKS * 2 * N) + 15) & ~(uintptr_t)15);
+  const int rc = linear_bnin_launch(M, N, K, a, a_mean, a_rstd, a_w, a_b, w, y, part, stream);
+  if (rc) return rc;
+  const int64_t chunk = (nparts + LBS_CHUNKS - 1) / LBS_CHUNKS;
+  const int nch = (int)((nparts + chunk - 1) / chunk);
+  hipLaunchKernelGGL(rowchunk_sum_kernel, dim3((2 * N + 31) / 32, nch), dim3(256), 0, stream, part, nparts, 2 * N,
+                     chunk, part2);
+  SM_CHECK_LAUNCH();
+  return sm_bn_stats_from_partials(part2, nch, N, M, mean, rstd, run_mean, run_var, num_batches_tracked, momentum,
+                                   eps, updates, fin, 2 * (int64_t)N * 8, stream);
+}
+
 extern "C" int64_t sm_linear_dw_se_workspace_bytes(int rows, int nout, int nin) {
   const int s = choose_splits(nout, nin, rows, true);
   return s > 1 ? (int64_t)s * nout * nin * 4 : 16;
@@ -1552,14 +1638,16 @@ extern "C" int sm_linear_dw_se(int rows, int nout, int nin, const void* dy, cons
                                hipStream_t stream) {
   if (nout <= 0 || nin <= 0 || rows <= 0) return 0;
   if (ws_bytes < sm_linear_dw_se_workspace_bytes(rows, nout, nin)) return -4;
-  if (nout % 8 || nin % 8 || hw <= 0 || hw % BKT || rows % hw || (((uintptr_t)dy | (uintptr_t)a2) & 15)) return -2;
+  if (nout % 8 || nin % 8 || (((uintptr_t)dy | (uintptr_t)a2) & 15)) return -2;
+  if (gate != nullptr && (hw <= 0 || hw % BKT || rows % hw)) return -2;   // no gate: any rows (x = BN(a2))
+  if (act_mean == nullptr) return -2;
   const int v = gemm_variant(nout, nin, rows);
   if (v == 1) return -2;
   GemmArgs g{};
   g.M = nout; g.N = nin; g.K = rows; g.A = dy; g.lda = nout; g.B = a2; g.ldb = nin; g.C = dW; g.ldc = nin;
   g.alpha = 1.f; g.beta = accumulate ? 1.f : 0.f; g.rows_per_group = 1;
   g.xb_act = ChanAffine{act_mean, act_rstd, act_w, act_b, act_gelu};
-  g.xb_gate = gate; g.xb_hw = hw;
+  g.xb_gate = gate; g.xb_hw = gate ? hw : 1;
   int splits = choose_splits(nout, nin, rows, true);
   if (splits > 1) {
     int chunk = (rows + splits - 1) / splits;

@@ -405,7 +405,7 @@ template <typename TI, typename TO>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const TI* x, const float* mean, const float* rstd,
                                                        const float* w, const float* b, TO* y, int64_t M, int C,
                                                        int rows_per_block, int gelu, const TO* R,
-                                                       const float* row_scale, int64_t rpg) {
+                                                       const float* row_scale, int64_t rpg, ChanAffine raff) {
   Col8 cm(C);
   if (!cm.active()) return;
   float sc[8], sh[8];
@@ -413,8 +413,12 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const TI* x, const float*
   for (int j = 0; j < 8; ++j) {
     const int c = cm.chunk * 8 + j;
     sc[j] = rstd[c] * w[c];
-    sh[j] = b[c] - mean[c] * sc[j];
+    sh[j] = bn_shift(b[c], mean[c], sc[j]);
   }
+  // residual stored pre-BatchNorm (raff.mean != null): R's value is the BN output
+  // bf16(R * rsc + rsh) exactly as bn_apply would have stored it (no GELU)
+  Affine8 ra;
+  ra.init(raff, cm.chunk * 8);
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = min(M, r0 + rows_per_block);
   for (int64_t row = r0 + cm.r; row < r1; row += cm.rpp) {
@@ -436,6 +440,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const TI* x, const float*
     if (R) {
       float rr[8];
       load8(R + e, rr);
+      ra.apply<TO>(rr);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] += rr[j];
     }
@@ -909,7 +914,31 @@ extern "C" int sm_bn_apply(int x_dtype, int y_dtype, int64_t M, int C, const voi
   DISPATCH2(x_dtype, y_dtype,
             hipLaunchKernelGGL((bn_apply_kernel<T1, T2>), dim3(nb), dim3(256), 0, st, (const T1*)x,
                                mean, rstd, w, b, (T2*)y, M, C, rpb, gelu, (const T2*)R, row_scale,
-                               rows_per_group > 0 ? rows_per_group : 1));
+                               rows_per_group > 0 ? rows_per_group : 1, ChanAffine{}));
+  SM_CHECK_LAUNCH();
+  return 0;
+}
+
+// sm_bn_apply with the residual R stored before its own BatchNorm (the stem's conv2 output
+// a2 when BN2's apply is folded into stage 0's consumers): R's value is bf16(R * r_sc +
+// r_sh) with r_sc = r_rstd * r_w, r_sh = r_b - r_mean * r_sc, exactly as sm_bn_apply stores
+// the BN output, so y is bit-identical to sm_bn_apply(.., R = sm_bn_apply(R, r_*)).
+extern "C" int sm_bn_apply_res_bn(int x_dtype, int y_dtype, int64_t M, int C, const void* x, const float* mean,
+                                  const float* rstd, const float* w, const float* b, void* y, int gelu,
+                                  const void* R, const float* r_mean, const float* r_rstd, const float* r_w,
+                                  const float* r_b, const float* row_scale, int64_t rows_per_group,
+                                  hipStream_t st) {
+  if (M <= 0) return 0;
+  if (C % 8 || C / 8 > 256 || R == nullptr || r_mean == nullptr || r_rstd == nullptr || r_w == nullptr ||
+      r_b == nullptr)
+    return -2;
+  const int rpb = stream_rows_per_block(M);
+  const int nb = (int)((M + rpb - 1) / rpb);
+  const ChanAffine raff{r_mean, r_rstd, r_w, r_b, 0};
+  DISPATCH2(x_dtype, y_dtype,
+            hipLaunchKernelGGL((bn_apply_kernel<T1, T2>), dim3(nb), dim3(256), 0, st, (const T1*)x,
+                               mean, rstd, w, b, (T2*)y, M, C, rpb, gelu, (const T2*)R, row_scale,
+                               rows_per_group > 0 ? rows_per_group : 1, raff));
   SM_CHECK_LAUNCH();
   return 0;
 }

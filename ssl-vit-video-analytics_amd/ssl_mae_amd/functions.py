@@ -96,7 +96,14 @@ def _train_bn_only(ctx, *bns):
 class StemFn(torch.autograd.Function):
     """PatchEmbed (tiny_vit.py:62-72): conv3x3 s2 3->48, BN, GELU, conv3x3 s1 48->96, BN.
     Input: the clip [B,3,T,H,W] (or frames [N,3,H,W]); the frame permute of
-    mae_vit_adapter.py:84 is folded into the im2col loads."""
+    mae_vit_adapter.py:84 is folded into the im2col loads.
+
+    Outputs (t, m2, r2).  With st.fold_bn2 (bf16 training, direct conv2 path) BN2's apply
+    is folded into stages[0][0], its only consumer: t holds the conv2 output a2, NOT y =
+    BN2(a2), and (m2, r2) are BN2's batch statistics; the consumer (MBConvFn with
+    st.x_bn) forms y = bf16(a2 sc + sh) in its own loads exactly as bn_apply stores it
+    and returns dL/dy as t's gradient, so y never exists in HBM.  Otherwise t = y and
+    (m2, r2) are returned for reference only."""
 
     @staticmethod
     def forward(ctx, clip, st, w1, g1, b1, w2, g2, b2):
@@ -112,7 +119,8 @@ class StemFn(torch.autograd.Function):
                 # statistics
                 a2, m2, r2 = K.stem_conv2_bn_stats(a1, (m1, r1, g1.detach(), b1.detach(), True), w2p, Fr, Ho, Wo,
                                                    st.bn2)
-                y = K.bn_apply(a2, m2, r2, g2.detach(), b2.detach(), gelu=False)
+                y = a2 if st.fold_bn2 else K.bn_apply(a2, m2, r2, g2.detach(), b2.detach(), gelu=False)
+                ctx.folded = st.fold_bn2
             else:
                 h1 = K.bn_apply(a1, m1, r1, g1.detach(), b1.detach(), gelu=True)
         else:
@@ -136,14 +144,17 @@ class StemFn(torch.autograd.Function):
                 del col2
             del h1
             y, m2, r2 = _bn_forward(a2, st.bn2, gelu=False)
+        if not getattr(ctx, "folded", False):
+            ctx.folded = False
         ctx.st = st
         ctx.geom = (Fr, Ho, Wo)
         ctx.params = (w1, g1, b1, w2, g2, b2)
         ctx.save_for_backward(clip, a1, a2, m1, r1, m2, r2, w1p, w2p)
-        return y.view(Fr, Ho, Wo, 96)
+        ctx.mark_non_differentiable(m2, r2)
+        return y.view(Fr, Ho, Wo, 96), m2, r2
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, _dm2=None, _dr2=None):
         _train_bn_only(ctx, ctx.st.bn1, ctx.st.bn2)
         clip, a1, a2, m1, r1, m2, r2, w1p, w2p = ctx.saved_tensors
         w1, g1, b1, w2, g2, b2 = ctx.params
@@ -191,7 +202,11 @@ class MBConvFn(torch.autograd.Function):
     st.recompute_a2: also drop the depthwise output a2 and recompute it in the
     backward from a1 with the saved BN0 statistics (no running-stat update) -- the
     stage-0 "lite-resident" mode: two recomputed kernels instead of the whole
-    checkpointed stage forward."""
+    checkpointed stage forward.
+    st.x_bn = (mean, rstd, weight, bias): the input is stored before its BatchNorm (the
+    stem's conv2 output under StemFn's folded BN2): every read of x -- the expand conv's
+    A operand, the residual, the expand weight gradient's B operand -- forms bf16(BN(x))
+    in its loads, bit-identical to reading the stored BN output."""
 
     @staticmethod
     def forward(ctx, x, st, w_exp, g0, b0, w_dw, g2, b2, w_fc0, w_fc2, w_proj, g5, b5):
@@ -201,7 +216,16 @@ class MBConvFn(torch.autograd.Function):
         x2d = x.reshape(-1, Cin)
         Ho, Wo = (H - 1) // s + 1, (Wd - 1) // s + 1
         fused = mode.bf16 and mid % 32 == 0
-        if fused and st.bn0.training:   # expand conv + BN0 statistics from its epilogue
+        xbn = getattr(st, "x_bn", None)
+        if xbn is not None:            # x = bf16(BN(stored)) formed in the expand GEMM's loads
+            if not fused:
+                raise NotImplementedError("a BatchNorm-folded input needs the fused bf16 MBConv")
+            xbn = tuple(xbn[:4]) + (False,)
+            if st.bn0.training:
+                a1, m0, r0 = K.linear_bnin(x2d, xbn, W(w_exp, mode).view(mid, Cin), st.bn0, st.bn_updates)
+            else:
+                a1 = K.linear_bnin(x2d, xbn, W(w_exp, mode).view(mid, Cin))
+        elif fused and st.bn0.training:   # expand conv + BN0 statistics from its epilogue
             a1, m0, r0 = K.linear_bn_stats(x2d, W(w_exp, mode).view(mid, Cin), st.bn0, st.bn_updates)
         else:
             a1 = K.linear(x2d, W(w_exp, mode).view(mid, Cin))
@@ -239,9 +263,11 @@ class MBConvFn(torch.autograd.Function):
         del h3
         mean5, rstd5 = _bn_params(a3, st.bn5, st.bn_updates)
         out = K.bn_apply(a3, mean5, rstd5, g5.detach(), b5.detach(), residual=x2d if st.res else None,
-                         row_scale=st.dp_scale, rows_per_group=Ho * Wo)
+                         row_scale=st.dp_scale, rows_per_group=Ho * Wo,
+                         residual_bn=xbn if (st.res and xbn is not None) else None)
         m5, r5 = mean5, rstd5
         ctx.fused = fused
+        ctx.xbn = xbn
         ctx.st = st
         ctx.geom = (Fr, H, Wd, Cin, Ho, Wo)
         ctx.params = (w_exp, g0, b0, w_dw, g2, b2, w_fc0, w_fc2, w_proj, g5, b5)
@@ -260,8 +286,14 @@ class MBConvFn(torch.autograd.Function):
         Fr, H, Wd, Cin, Ho, Wo = ctx.geom
         mid, Cout, s = st.mid, st.cout, st.stride
         _touch(*ctx.params)
+        xbn = ctx.xbn
+
+        def expand(xin):        # recompute a1 = x W^T (same kernel form as the forward's)
+            if xbn is not None:
+                return K.linear_bnin(xin.reshape(-1, Cin), xbn, W(w_exp, mode).view(mid, Cin))
+            return K.linear(xin.reshape(-1, Cin), W(w_exp, mode).view(mid, Cin))
         if a2 is None:          # lite-resident: a1 and a2 recomputed from x (same kernels, saved stats)
-            a1 = K.linear(x.reshape(-1, Cin), W(w_exp, mode).view(mid, Cin))
+            a1 = expand(x)
             if ctx.fused:
                 a2 = K.dwconv_fused(a1, (m0, r0, g0.detach(), b0.detach(), True), w_dw.detach().view(mid, 9), Fr,
                                     H, Wd, mid, s)
@@ -302,7 +334,7 @@ class MBConvFn(torch.autograd.Function):
         K.gemm(dz2, h1se, G(w_fc2), mid, R, Fr, 1, 1, mid, R, R, beta=1.0)
         K.gemm(dz1, pooled, G(w_fc0), R, mid, Fr, 1, 1, R, mid, mid, beta=1.0)
         if a1 is None:
-            a1 = K.linear(x.reshape(-1, Cin), W(w_exp, mode).view(mid, Cin))
+            a1 = expand(x)
         if ctx.fused:
             # depthwise + BN0/GELU backward in two passes over (da2, a1); dh1 never stored
             act0 = (m0, r0, g0.detach(), b0.detach(), True)
@@ -318,7 +350,10 @@ class MBConvFn(torch.autograd.Function):
             da1 = K.bn_bwd(dh1, a1, m0, r0, g0.detach(), b0.detach(), True, G(g0), G(b0))
             del dh1
         x2d = x.reshape(-1, Cin)
-        K.linear_dw(da1, x2d, G(w_exp).view(mid, Cin))
+        if xbn is not None:     # B operand bf16(BN(x)) formed on load (no gate)
+            K.linear_dw_se(da1, x2d, xbn, None, 0, G(w_exp).view(mid, Cin))
+        else:
+            K.linear_dw(da1, x2d, G(w_exp).view(mid, Cin))
         dx = K.linear_dx(da1, W(w_exp, mode).view(mid, Cin), residual=dout2d if st.res else None)
         _done(*ctx.params)
         return (dx.view(Fr, H, Wd, Cin),) + (None,) * 12

@@ -142,6 +142,31 @@ def linear_bn_stats(x, w, running_mean=None, running_var=None, momentum=0.1, eps
     return y, mean, rstd
 
 
+def linear_bnin(a, act, w, bn=None, updates=1):
+    """y [M,N] bf16 = x @ w^T with x = bf16(BN(a)) (act = (mean, rstd, weight, bias), no GELU)
+    formed in the GEMM's A-operand loads (sm_linear_bnin; bit-identical to bn_apply +
+    linear).  bn: also the train-mode BatchNorm statistics of y (sm_linear_bnin_bn_stats,
+    = linear_bn_stats); returns y, or (y, mean, rstd) with bn."""
+    _chk(a, w, *act[:4])
+    M, Kd = a.shape
+    N = w.shape[0]
+    if w.shape[1] != Kd or a.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or act[4]:
+        raise _lib.KernelError("linear_bnin: bf16 a [M,K], w [N,K], BatchNorm act without GELU")
+    y = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    if bn is None:
+        call("sm_linear_bnin", M, N, Kd, ptr(a), *[ptr(t) for t in act[:4]], ptr(w), ptr(y), stream())
+        return y
+    running_mean, running_var, momentum, eps, num_batches = bn
+    mean = torch.empty(N, dtype=torch.float32, device=a.device)
+    rstd = torch.empty(N, dtype=torch.float32, device=a.device)
+    nbytes = query("sm_linear_bn_stats_workspace_bytes", M, N)
+    ws = _ws(nbytes, a.device)
+    call("sm_linear_bnin_bn_stats", M, N, Kd, ptr(a), *[ptr(t) for t in act[:4]], ptr(w), ptr(y), ptr(mean),
+         ptr(rstd), ptr(running_mean), ptr(running_var), ptr(num_batches), float(momentum), float(eps), int(updates),
+         ptr(ws), nbytes, stream())
+    return y, mean, rstd
+
+
 def linear_se(a2, w, act, gate, hw):
     """y [M,N] bf16 = h3 @ w^T with h3 = se_scale(a2, gate, act) formed in the GEMM's
     A-operand loads (sm_linear_se; bit-identical to se_fwd's h3 + linear).  a2 [M,C] bf16,
@@ -161,15 +186,20 @@ def linear_dw_se(dy, a2, act, gate, hw, grad_sink, accumulate=True):
     """grad_sink[N,C] (+)= dy^T @ h3 with h3 = se_scale(a2, gate, act) formed in the GEMM's
     operand loads (sm_linear_dw_se; bit-identical to se_scale + linear_dw).  dy [M,N],
     a2 [M,C] bf16, gate [M/hw, C] fp32, hw % 64 == 0."""
-    _chk(dy, a2, gate, grad_sink)
+    _chk(dy, a2, grad_sink)
     M, N = dy.shape
     C = a2.shape[1]
-    if a2.shape[0] != M or gate.shape != (M // hw, C) or M % hw or grad_sink.shape != (N, C):
+    if gate is None:          # B = the BatchNorm output act(a2) itself (the stem's BN2, no gate)
+        hw = 1
+    elif gate.shape != (M // hw, C) or M % hw:
+        raise _lib.KernelError("linear_dw_se: gate shape mismatch")
+    if a2.shape[0] != M or grad_sink.shape != (N, C):
         raise _lib.KernelError("linear_dw_se: shape mismatch")
     nbytes = query("sm_linear_dw_se_workspace_bytes", M, N, C)
     ws = _ws(nbytes, dy.device)
-    call("sm_linear_dw_se", M, N, C, ptr(dy), ptr(a2), *_act_args(act), ptr(gate.contiguous()), int(hw),
-         ptr(grad_sink), 1 if accumulate else 0, ptr(ws), nbytes, stream())
+    call("sm_linear_dw_se", M, N, C, ptr(dy), ptr(a2), *_act_args(act),
+         ptr(None if gate is None else gate.contiguous()), int(hw), ptr(grad_sink), 1 if accumulate else 0,
+         ptr(ws), nbytes, stream())
     return grad_sink
 
 
@@ -266,9 +296,19 @@ def bn_eval_params(bn):
     return mean, rstd
 
 
-def bn_apply(x2d, mean, rstd, w, b, gelu=False, out_dtype=None, residual=None, row_scale=None, rows_per_group=1):
+def bn_apply(x2d, mean, rstd, w, b, gelu=False, out_dtype=None, residual=None, row_scale=None, rows_per_group=1,
+             residual_bn=None):
+    """residual_bn = (mean, rstd, weight, bias): the residual is stored before its own
+    BatchNorm and enters as bf16(BN(residual)) (sm_bn_apply_res_bn)."""
     M, C = x2d.shape
     y = torch.empty((M, C), dtype=out_dtype or x2d.dtype, device=x2d.device)
+    if residual_bn is not None:
+        if residual is None:
+            raise _lib.KernelError("bn_apply: residual_bn without a residual")
+        call("sm_bn_apply_res_bn", dt(x2d), dt(y), M, C, ptr(x2d), ptr(mean), ptr(rstd), ptr(w), ptr(b), ptr(y),
+             1 if gelu else 0, ptr(residual), *[ptr(t) for t in residual_bn[:4]], ptr(row_scale), int(rows_per_group),
+             stream())
+        return y
     call("sm_bn_apply", dt(x2d), dt(y), M, C, ptr(x2d), ptr(mean), ptr(rstd), ptr(w), ptr(b), ptr(y),
          1 if gelu else 0, ptr(residual), ptr(row_scale), int(rows_per_group), stream())
     return y

@@ -359,7 +359,15 @@ _bn_apply.register_fake(lambda x, mean, rstd, w, b, gelu, out_dtype, *a: x.new_e
                                                                                      dtype=out_dtype or x.dtype))
 
 
-def bn_apply(x2d, mean, rstd, w, b, gelu=False, out_dtype=None, residual=None, row_scale=None, rows_per_group=1):
+def bn_apply(x2d, mean, rstd, w, b, gelu=False, out_dtype=None, residual=None, row_scale=None, rows_per_group=1,
+             residual_bn=None):
+    """residual_bn = (mean, rstd, weight, bias[, gelu False]): the residual is stored before
+    its own BatchNorm (the stem's a2 under stages[0][0]) and enters as bf16(BN(residual))."""
+    if residual_bn is not None:
+        if len(residual_bn) > 4 and residual_bn[4]:
+            raise ValueError("bn_apply: the residual's BatchNorm has no GELU")
+        return torch.ops.ssl_mae.bn_apply_res_bn(x2d, mean, rstd, w, b, bool(gelu), out_dtype, residual,
+                                                 *residual_bn[:4], row_scale, int(rows_per_group))
     return torch.ops.ssl_mae.bn_apply(x2d, mean, rstd, w, b, bool(gelu), out_dtype, residual, row_scale,
                                       int(rows_per_group))
 
@@ -863,6 +871,57 @@ def linear_bn_stats(x, w, bn, updates=1):
                                              float(bn.eps), int(updates), bn.num_batches_tracked)
 
 
+@_op("linear_bnin", "(Tensor a, Tensor a_mean, Tensor a_rstd, Tensor a_w, Tensor a_b, Tensor w) -> Tensor")
+def _linear_bnin(a, am, ar, aw, ab, w):
+    return _K.linear_bnin(a, (am, ar, aw, ab, False), w)
+
+
+_linear_bnin.register_fake(lambda a, am, ar, aw, ab, w: a.new_empty((a.shape[0], w.shape[0]), dtype=torch.bfloat16))
+
+
+@_op("linear_bnin_bn_stats", "(Tensor a, Tensor a_mean, Tensor a_rstd, Tensor a_w, Tensor a_b, Tensor w, "
+                             "Tensor(a!)? running_mean, Tensor(b!)? running_var, float momentum, float eps, "
+                             "int updates, Tensor(c!)? num_batches_tracked) -> (Tensor, Tensor, Tensor)",
+     ("running_mean", "running_var", "num_batches_tracked"))
+def _linear_bnin_bn_stats(a, am, ar, aw, ab, w, running_mean, running_var, momentum, eps, updates,
+                          num_batches_tracked):
+    return _K.linear_bnin(a, (am, ar, aw, ab, False), w,
+                          (running_mean, running_var, momentum, eps, num_batches_tracked), updates)
+
+
+@_linear_bnin_bn_stats.register_fake
+def _(a, am, ar, aw, ab, w, *rest):
+    N = w.shape[0]
+    return (a.new_empty((a.shape[0], N), dtype=torch.bfloat16), a.new_empty(N, dtype=torch.float32),
+            a.new_empty(N, dtype=torch.float32))
+
+
+def linear_bnin(a, act, w, bn=None, updates=1):
+    """Linear (1x1 conv) over the BatchNorm output x = bf16(BN(a)) formed in the GEMM's
+    operand loads (act = (mean, rstd, weight, bias, False): the stem's BN2 feeding
+    stages[0][0]); with bn (the consumer's BatchNorm2d module) also that BatchNorm's
+    train-mode statistics from the epilogue (-> (y, mean, rstd))."""
+    if act[4]:
+        raise ValueError("linear_bnin: the folded BatchNorm has no GELU")
+    if bn is None:
+        return torch.ops.ssl_mae.linear_bnin(a, *act[:4], w)
+    return torch.ops.ssl_mae.linear_bnin_bn_stats(a, *act[:4], w, bn.running_mean, bn.running_var,
+                                                  float(bn.momentum), float(bn.eps), int(updates),
+                                                  bn.num_batches_tracked)
+
+
+@_op("bn_apply_res_bn", "(Tensor x, Tensor mean, Tensor rstd, Tensor w, Tensor b, bool gelu, ScalarType? out_dtype, "
+                        "Tensor residual, Tensor r_mean, Tensor r_rstd, Tensor r_w, Tensor r_b, Tensor? row_scale, "
+                        "int rows_per_group) -> Tensor")
+def _bn_apply_res_bn(x, mean, rstd, w, b, gelu, out_dtype, residual, rm, rr, rw, rb, row_scale, rows_per_group):
+    return _K.bn_apply(x, mean, rstd, w, b, gelu, out_dtype, residual, row_scale, rows_per_group,
+                       residual_bn=(rm, rr, rw, rb))
+
+
+_bn_apply_res_bn.register_fake(lambda x, mean, rstd, w, b, gelu, out_dtype, *a: x.new_empty(x.shape,
+                                                                                           dtype=out_dtype or x.dtype))
+
+
 @_op("linear_se", "(Tensor a2, Tensor w, Tensor act_mean, Tensor act_rstd, Tensor act_w, Tensor act_b, "
                   "bool act_gelu, Tensor gate, int hw) -> Tensor")
 def _linear_se(a2, w, am, ar, aw, ab, ag, gate, hw):
@@ -878,7 +937,7 @@ def linear_se(a2, w, act, gate, hw):
 
 
 @_op("linear_dw_se", "(Tensor dy, Tensor a2, Tensor act_mean, Tensor act_rstd, Tensor act_w, Tensor act_b, "
-                     "bool act_gelu, Tensor gate, int hw, Tensor(a!) grad_sink, bool accumulate) -> ()", ("grad_sink",))
+                     "bool act_gelu, Tensor? gate, int hw, Tensor(a!) grad_sink, bool accumulate) -> ()", ("grad_sink",))
 def _linear_dw_se(dy, a2, am, ar, aw, ab, ag, gate, hw, grad_sink, accumulate):
     _K.linear_dw_se(dy, a2, (am, ar, aw, ab, ag), gate, hw, grad_sink, accumulate)
 

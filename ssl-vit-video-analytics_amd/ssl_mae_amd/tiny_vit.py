@@ -81,12 +81,12 @@ class MBConv(nn.Module):
             Conv2d_BN(mid, out_chans, ks=1, bn_weight_init=0))
         self.drop_path = DropPath(drop_path) if drop_path > 0.0 else nn.Identity()
 
-    def run(self, x, mode, resident=False):
+    def run(self, x, mode, resident=False, x_bn=None):
         c = self.conv
         dps = droppath_scale(self, x.shape[0], mode, 0, x.device) if self.use_res_connect else None
         st = _St(mode=mode, mid=self.mid, cout=self.out_chans, stride=self.stride, res=self.use_res_connect,
                  bn0=c[0].bn, bn2=c[2].bn, bn5=c[5].bn, dp_scale=dps, bn_updates=2 if resident else 1,
-                 recompute_a1=bool(resident), recompute_a2=resident == "lite")
+                 recompute_a1=bool(resident), recompute_a2=resident == "lite", x_bn=x_bn)
         return MBConvFn.apply(x, st, c[0].c.weight, c[0].bn.weight, c[0].bn.bias, c[2].c.weight, c[2].bn.weight,
                               c[2].bn.bias, c[4].fc[0].weight, c[4].fc[2].weight, c[5].c.weight, c[5].bn.weight,
                               c[5].bn.bias)
@@ -101,13 +101,23 @@ class PatchEmbed(nn.Module):
             Conv2d_BN(in_chans, embed_dim // 2, ks=3, stride=2, pad=1), nn.GELU(),
             Conv2d_BN(embed_dim // 2, embed_dim, ks=3, stride=1, pad=1))
 
+    # BN2's apply folded into stages[0][0] when the stem runs its direct conv2 (bf16
+    # training): False keeps the stored y = BN2(a2) (bit-identical either way)
+    fold_bn2 = True
+
     def run(self, clip, mode):
+        """-> (t, x_bn): t the stem output, or with x_bn = (mean, rstd, weight, bias) of BN2
+        the conv2 output a2 that stages[0][0] reads as bf16(BN2(a2)) (StemFn)."""
         pe = self.patch_embed
         if pe[0].c.weight.shape[:2] != (48, 3) or pe[2].c.weight.shape[:2] != (96, 48):
             raise NotImplementedError("fused stem is specialised for 3->48->96 (embed_dims[0]=96)")
-        st = _St(mode=mode, bn1=pe[0].bn, bn2=pe[2].bn)
-        return StemFn.apply(clip, st, pe[0].c.weight, pe[0].bn.weight, pe[0].bn.bias, pe[2].c.weight,
-                            pe[2].bn.weight, pe[2].bn.bias)
+        bn1, bn2 = pe[0].bn, pe[2].bn
+        wo = (clip.shape[-1] - 1) // 2 + 1
+        fold = bool(self.fold_bn2) and mode.bf16 and bn1.training and bn2.training and wo <= 128
+        st = _St(mode=mode, bn1=bn1, bn2=bn2, fold_bn2=fold)
+        t, m2, r2 = StemFn.apply(clip, st, pe[0].c.weight, bn1.weight, bn1.bias, pe[2].c.weight, bn2.weight,
+                                 bn2.bias)
+        return t, ((m2, r2, bn2.weight.detach(), bn2.bias.detach()) if fold else None)
 
 
 class Mlp(nn.Module):
@@ -161,9 +171,14 @@ class TinyViTBlock(nn.Module):
 
 
 class _Stage(nn.Sequential):
-    def run(self, x, mode, resident=False):
-        for blk in self:
-            x = blk.run(x, mode, resident)
+    def run(self, x, mode, resident=False, x_bn=None):
+        """x_bn: x is stored before its BatchNorm (stage 0 under the stem's folded BN2):
+        only the first block reads it."""
+        for i, blk in enumerate(self):
+            if i == 0 and x_bn is not None:
+                x = blk.run(x, mode, resident, x_bn=x_bn)
+            else:
+                x = blk.run(x, mode, resident)
         return x
 
 
@@ -208,7 +223,7 @@ class TinyViT(nn.Module):
         from .mae_vit_adapter import next_seed_base
         return Mode(torch.is_autocast_enabled("cuda"), next_seed_base(self))
 
-    def _run_stages(self, x, n_stages, mode):
+    def _run_stages(self, x, n_stages, mode, x_bn=None):
         """tiny_vit.py:170-175: each stage under checkpoint(use_reentrant=False) when
         training with use_checkpoint.  A stage listed in resident_stages keeps its
         activations in HBM instead (288 GB holds them at the bench batch): no
@@ -232,21 +247,22 @@ class TinyViT(nn.Module):
                 if self.use_checkpoint and self.training and grad else ()
         for i in range(n_stages):
             stage = self.stages[i]
+            xb = x_bn if i == 0 else None
             if self.use_checkpoint and self.training and grad:
                 if i in resident:
-                    x = stage.run(x, mode, resident=True)
+                    x = stage.run(x, mode, True, xb)
                 elif i in lite:
-                    x = stage.run(x, mode, resident="lite")
+                    x = stage.run(x, mode, "lite", xb)
                 else:
-                    x = checkpoint.checkpoint(stage.run, x, mode, use_reentrant=False)
+                    x = checkpoint.checkpoint(stage.run, x, mode, False, xb, use_reentrant=False)
             else:
-                x = stage.run(x, mode)
+                x = stage.run(x, mode, False, xb)
         return x
 
     def tokens_stage3(self, clip, mode):
         """clip [B,3,T,H,W] or frames [N,3,H,W] -> channels-last [N*T, H/8, W/8, 384]."""
-        x = self.patch_embed.run(clip, mode)
-        return self._run_stages(x, 3, mode)
+        x, x_bn = self.patch_embed.run(clip, mode)
+        return self._run_stages(x, 3, mode, x_bn)
 
     def _prepare(self, mode):
         from .mae_vit_adapter import ensure_flat
@@ -263,8 +279,8 @@ class TinyViT(nn.Module):
     def tokens_all(self, x, mode):
         """All four stages, channels-last: frames [N,3,H,W] (any strides) or a clip
         [B,3,T,H,W] (frames b*T + t) -> [N, H/16, W/16, C4]."""
-        t = self.patch_embed.run(x, mode)
-        return self._run_stages(t, 4, mode)
+        t, x_bn = self.patch_embed.run(x, mode)
+        return self._run_stages(t, 4, mode, x_bn)
 
     def forward(self, x):
         """All four stages (tiny_vit.py:178-186) -> [N, C4, H/16, W/16] (NCHW view)."""
