@@ -62,27 +62,34 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(T, S, ratio):
+def cpu_baseline(T, S, ratio, B=4):
     """The CPU oracle (fp32 restatement of the reference path) timed on the host
-    cores: ONE clip, one fwd+bwd+AdamW step (bounded sample, ~10-30 s)."""
+    cores at BASELINE config 1's batch: one fwd+bwd+AdamW step of B = 4 clips (the
+    reference's C1 step, train_ssl_mae.py:66-91; bounded sample, ~30 s)."""
     from oracle import mae_oracle as O
     from ssl_mae_amd.init_rule import param_value, synthetic_clip
     cfg = {"dataset": {"clip_len": T, "image_size": S},
            "model": {"decoder_embed_dim": 384, "decoder_depth": 4, "decoder_num_heads": 6},
            "ssl": {"mask_ratio": ratio, "norm_pix_loss": True}}
     threads = torch.get_num_threads()
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
     P = O.make_params(cfg, param_value)
     bufs = O.init_buffers(P)
     opt = O.AdamWState(lr=5e-4)
-    clip = torch.from_numpy(synthetic_clip(1, T, S, seed=7))
+    clip = torch.from_numpy(synthetic_clip(B, T, S, seed=7))
     torch.manual_seed(42)
-    mask = O.get_tube_mask(1, T, (S // 8) ** 2, ratio)
+    mask = O.get_tube_mask(B, T, (S // 8) ** 2, ratio)
     t0 = time.perf_counter()
     O.train_step(P, bufs, opt, clip, mask, cfg)
     dt = time.perf_counter() - t0
-    return {"value": round(1.0 / dt, 5), "unit": "clips/s", "cores": threads, "kind": "port",
-            "sample": f"1 clip {T}x3x{S}x{S}, one fp32 fwd+bwd+AdamW step of oracle/mae_oracle.py "
-                      f"(dropout off) on {threads} host threads; {dt:.1f} s"}
+    return {"value": round(B / dt, 5), "unit": "clips/s", "cores": threads, "threads": threads,
+            "nproc": os.cpu_count(), "affinity_cpus": affinity, "kind": "port",
+            "sample": f"BASELINE config 1 step: {B} clips {T}x3x{S}x{S}, one fp32 fwd+bwd+AdamW step of "
+                      f"oracle/mae_oracle.py (dropout off) on {threads} torch threads (nproc {os.cpu_count()}, "
+                      f"affinity {affinity}); {dt:.1f} s"}
 
 
 PROBE_KERNELS = {"dec_attn_fwd": "attn_fwd_bf16<64, true>",

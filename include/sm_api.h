@@ -118,8 +118,12 @@ int sm_linear_dw_se(int rows, int nout, int nin, const void* dy, const void* a2,
  * qkv packed [N][L][3][H][D] bf16|f32, out O [N][L][H][D], lse [N][H][L]. */
 int sm_attn_fwd(int dtype, int N, int L, int H, int D, const void* qkv, void* out, float* lse,
                 float scale, float drop_p, uint64_t seed, hipStream_t st);
+/* delta_ws: workspace of sm_attn_bwd_workspace_bytes (256-B aligned): rowsum(dO * O)
+ * [N][H][L] fp32, then for bf16 the dQ kernel's bf16(Q * scale * log2 e) [N][L][H][D], the
+ * operand the dK/dV kernel's scores are formed from (the forward's and dQ's S exactly). */
+int64_t sm_attn_bwd_workspace_bytes(int dtype, int N, int L, int H, int D);
 int sm_attn_bwd(int dtype, int N, int L, int H, int D, const void* qkv, const void* o,
-                const void* dout, const float* lse, float* delta_ws /*[N][H][L]*/, void* dqkv,
+                const void* dout, const float* lse, float* delta_ws, void* dqkv,
                 float scale, float drop_p, uint64_t seed, hipStream_t st);
 
 /* ---- LayerNorm (tiny_vit.py:112,115; decoder norm1/norm2; mae_vit_adapter.py:50) */

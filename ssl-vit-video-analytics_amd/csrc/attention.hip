@@ -41,6 +41,7 @@ struct AttnArgs {
   const void* dout;  // bwd: dO [N][L][H][D]
   float* lse;        // [N][H][L]
   float* delta;      // [N][H][L]  rowsum(dO * O)
+  __bf16* qc;        // bwd (bf16): bf16(Q * scale * log2 e) [N][L][H][D], written by the dQ kernel
   int N, L, H;
   float scale;
   float drop_p;      // dropout on attention probabilities (0 = off)
@@ -464,7 +465,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_bf16(AttnArgs a
   const int C = a.H * D;
   const int ldq = 3 * C;
   const __bf16* qkv = (const __bf16*)a.qkv + (int64_t)n * a.L * ldq;
-  const __bf16* qb = qkv + hd * D;
+  const __bf16* qb = a.qc + (int64_t)n * a.L * C + hd * D;   // bf16(Q * scale * log2 e), row stride C
   const __bf16* kb = qkv + C + hd * D;
   const __bf16* vb = qkv + 2 * C + hd * D;
   const __bf16* dob = (const __bf16*)a.dout + (int64_t)n * a.L * C + hd * D;
@@ -483,16 +484,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_bf16(AttnArgs a
       for (int j = 0; j < 8; ++j) { kf[s][j] = (__bf16)0.f; vf[s][j] = (__bf16)0.f; }
     }
   }
-  // K pre-scaled by scale * log2(e) (once, in registers) and the S accumulator started
-  // at -LSE2 of its query row: the MFMA leaves the exp2 argument itself, one VALU op per
-  // score fewer than exp2(fma(S, c, -LSE2)) (the kernels are bound by VALU issue).
-  // dK uses Q from LDS, unscaled.
-#pragma unroll
-  for (int s = 0; s < D / 16; ++s)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) kf[s][j] = (__bf16)((float)kf[s][j] * (a.scale * LOG2E));
+  // The Q tiles are the dQ kernel's bf16(Q * scale * log2 e) (a.qc) and the S accumulator
+  // starts at -LSE2 of its query row: the MFMA leaves the exp2 argument itself (one VALU op
+  // per score fewer than exp2(fma(S, c, -LSE2))), and S is formed from exactly the rounded
+  // operand the forward and the dQ kernel use (bf16(Q c) . K), so the rebuilt P rows match
+  // the forward's normalisation.  dK = dS^T Q scale = dS^T Qc ln 2.
   Stager<D, QT, 64 * NW> sq, sd;
-  sq.init(ldq);
+  sq.init(C);
   sd.init(C);
   int roff[D / 16], tlo[D / 32], thi[D / 32];
 #pragma unroll
@@ -607,7 +605,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_bf16(AttnArgs a
     }
     __syncthreads();
     if (q0 + QT < a.L) {
-      sq.load(qb + (int64_t)(q0 + QT) * ldq, a.L - q0 - QT, rq);
+      sq.load(qb + (int64_t)(q0 + QT) * C, a.L - q0 - QT, rq);
       sd.load(dob + (int64_t)(q0 + QT) * C, a.L - q0 - QT, rd);
       rowc_load(q0 + QT);
     }
@@ -629,7 +627,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_bf16(AttnArgs a
       for (int g = 0; g < 4; ++g) {
         float vk[4], vv[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) { vk[i] = dk[t][4 * g + i] * a.scale; vv[i] = dv[t][4 * g + i]; }
+        for (int i = 0; i < 4; ++i) { vk[i] = dk[t][4 * g + i] * LN2; vv[i] = dv[t][4 * g + i]; }
         store4(out + C + 32 * t + 8 * g + 4 * h, vk);
         store4(out + 2 * C + 32 * t + 8 * g + 4 * h, vv);
       }
@@ -683,9 +681,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_bf16(AttnArgs a) 
   // Q pre-scaled by scale * log2(e) in registers and S started at -LSE2: the MFMA leaves
   // the exp2 argument (as in the dK/dV kernel); dQ = dS K needs no Q
 #pragma unroll
-  for (int s = 0; s < D / 16; ++s)
+  for (int s = 0; s < D / 16; ++s) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) qf[s][j] = (__bf16)((float)qf[s][j] * (a.scale * LOG2E));
+    // the same rounded operand for the dK/dV kernel's S (it runs after this one)
+    if (qok) *(bf16x8*)(a.qc + ((int64_t)n * a.L + q) * C + hd * D + 16 * s + 8 * h) = qf[s];
+  }
   Stager<D, KT, 64 * NW> stg;
   stg.init(ldq);
   int roff[D / 16], tlo[D / 32], thi[D / 32];
@@ -966,13 +967,22 @@ extern "C" int sm_attn_fwd(int dtype, int N, int L, int H, int D, const void* qk
   return 0;
 }
 
+// workspace of sm_attn_bwd: Delta [N][H][L] fp32, then (bf16) bf16(Q scale log2 e) [N][L][H][D]
+static int64_t attn_delta_bytes(int N, int L, int H) { return ((int64_t)N * H * L * 4 + 255) / 256 * 256; }
+extern "C" int64_t sm_attn_bwd_workspace_bytes(int dtype, int N, int L, int H, int D) {
+  if (N <= 0 || L <= 0) return 0;
+  return attn_delta_bytes(N, L, H) + (dtype == SM_BF16 ? (int64_t)N * L * H * D * 2 : 0);
+}
+
 extern "C" int sm_attn_bwd(int dtype, int N, int L, int H, int D, const void* qkv, const void* o,
                            const void* dout, const float* lse, float* delta_ws, void* dqkv,
                            float scale, float drop_p, uint64_t seed, hipStream_t st) {
   if (N <= 0 || L <= 0) return 0;
   if (D != 32 && D != 64) return -2;
+  if (((uintptr_t)delta_ws) & 255) return -2;
   AttnArgs a{};
   a.qkv = qkv; a.o = o; a.dout = dout; a.lse = (float*)lse; a.delta = delta_ws; a.out = dqkv;
+  a.qc = (__bf16*)((char*)delta_ws + attn_delta_bytes(N, L, H));
   a.N = N; a.L = L; a.H = H; a.scale = scale; a.drop_p = drop_p; a.seed = seed;
   dim3 grid((L + 127) / 128, H, N);
   const bool drop = drop_p > 0.f;

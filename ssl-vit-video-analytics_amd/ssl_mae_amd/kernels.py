@@ -224,8 +224,8 @@ def attn_fwd(qkv, N, L, H, D, drop_p=0.0, seed=0):
 def attn_bwd(qkv, o, do, lse, N, L, H, D, drop_p=0.0, seed=0):
     _chk(qkv, o, do, lse)
     dqkv = torch.empty_like(qkv)
-    delta = torch.empty((N, H, L), dtype=torch.float32, device=qkv.device)
-    call("sm_attn_bwd", dt(qkv), N, L, H, D, ptr(qkv), ptr(o), ptr(do), ptr(lse), ptr(delta), ptr(dqkv),
+    ws = _ws(query("sm_attn_bwd_workspace_bytes", dt(qkv), N, L, H, D), qkv.device)   # Delta (+ scaled Q)
+    call("sm_attn_bwd", dt(qkv), N, L, H, D, ptr(qkv), ptr(o), ptr(do), ptr(lse), ptr(ws), ptr(dqkv),
          1.0 / math.sqrt(D), float(drop_p), int(seed), stream())
     return dqkv
 
