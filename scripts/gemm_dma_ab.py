@@ -1,0 +1,65 @@
+"""Same-process A/B of the forward GEMM kernels (knob 'gemm_dma': register-staged v2 vs
+the LDS-DMA ring) at the step's K-major shapes, alternating the variants per repetition.
+
+python scripts/gemm_dma_ab.py [--reps 3] [--iters 5]
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "ssl-vit-video-analytics_amd")]
+
+import torch  # noqa: E402
+
+from ssl_mae_amd import kernels as K  # noqa: E402
+from gemm_ksweep import timeit  # noqa: E402
+
+B = 256
+SHAPES = [  # (name, M, N, K, bias, gelu, stats)
+    ("dec qkv fwd", B * 6272, 1152, 384, True, False, False),
+    ("dec fc1+gelu fwd", B * 6272, 1536, 384, True, True, False),
+    ("dec fc2 fwd", B * 6272, 384, 1536, True, False, False),
+    ("dec proj fwd", B * 6272, 384, 384, True, False, False),
+    ("s0 expand+stats", B * 8 * 12544, 384, 96, False, False, True),
+    ("s1 qkv fwd", B * 8 * 3136, 576, 192, True, False, False),
+    ("s1 fc1+gelu", B * 8 * 3136, 768, 192, True, True, False),
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--only", default="")
+    args = ap.parse_args()
+    for name, M, N, Kd, bias, gelu, stats in SHAPES:
+        if args.only and args.only not in name:
+            continue
+        x = torch.randn(M, Kd, device="cuda").to(torch.bfloat16)
+        w = (torch.randn(N, Kd, device="cuda") * 0.05).to(torch.bfloat16)
+        b = torch.randn(N, device="cuda") if bias else None
+        if stats:
+            fn = lambda: K.linear_bn_stats(x, w)  # noqa: E731
+        else:
+            fn = lambda: K.linear(x, w, b, gelu=gelu)  # noqa: E731
+        t = {0: [], 1: []}
+        outs = {}
+        for _ in range(args.reps):
+            for v in (0, 1):
+                K.set_tuning("gemm_dma", v)
+                t[v].append(timeit(fn, args.iters))
+                o = fn()
+                outs[v] = o[0] if isinstance(o, tuple) else o
+        K.set_tuning("gemm_dma", 0)
+        same = torch.equal(outs[0], outs[1])
+        f = 2.0 * M * N * Kd
+        t0, t1 = min(t[0]), min(t[1])
+        print(f"{name:18s} M={M} N={N} K={Kd}: v2 {t0:7.3f} ms ({f / t0 / 1e9:6.0f} TF/s) | dma {t1:7.3f} ms "
+              f"({f / t1 / 1e9:6.0f} TF/s)  {t0 / t1:5.2f}x  bit-identical {same}", flush=True)
+        del x, w, b, outs
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

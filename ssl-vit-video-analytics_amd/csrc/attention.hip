@@ -988,7 +988,7 @@ extern "C" int sm_attn_bwd(int dtype, int N, int L, int H, int D, const void* qk
   const bool drop = drop_p > 0.f;
   if (dtype == SM_BF16) {
     // dQ first: it forms Delta = rowsum(dO*O) in its prologue for the dK/dV kernel
-    static const int var = [] { const char* e = getenv("SM_ATTN_BWD_VAR"); return e ? atoi(e) : 0; }();
+    const int var = sm_tuning_get(SM_TUNE_ATTN_BWD);
     if (D == 32) { if (drop) launch_attn_bwd<32, true>(a, var, st); else launch_attn_bwd<32, false>(a, var, st); }
     else { if (drop) launch_attn_bwd<64, true>(a, var, st); else launch_attn_bwd<64, false>(a, var, st); }
   } else {

@@ -1016,3 +1016,28 @@ def test_dwconv_bn_bwd_vs_fp32(Fr, H, C, s):
     assert rel_err(da1, gx) < 2e-2 and rel_err(da1, da1_u) < 2e-2
     assert rel_err(dw_f, tw.grad) < 1e-2 and rel_err(dw_f, dw_u) < 1e-2
     assert rel_err(dg_f, tg.grad) < 2e-2 and rel_err(db_f, tb.grad) < 2e-2
+
+
+@pytest.mark.parametrize("M,N,Kd", [(1000, 1152, 384), (4096, 384, 96), (777, 136, 200), (25088, 384, 96)])
+def test_gemm_dma_ring_bit_identical(M, N, Kd):
+    """The LDS-DMA ring forward GEMM (gemm_bf16_dma, knob 'gemm_dma') against the register-
+    staged v2 kernel: the same MFMA chain in the same k order, so y = x w^T (+ bias, + the
+    BatchNorm statistics epilogue) is bit-identical; ragged M / N / K tails read zero."""
+    kk = KK()
+    x = rnd(M, Kd, dtype=torch.bfloat16, seed=300).to(DEV)
+    w = rnd(N, Kd, dtype=torch.bfloat16, seed=301, scale=0.3).to(DEV)
+    b = rnd(N, seed=302).to(DEV)
+    try:
+        kk.set_tuning("gemm_dma", 0)
+        y0 = kk.linear(x, w, b)
+        s0 = kk.linear_bn_stats(x, w) if Kd % 8 == 0 else None
+        kk.set_tuning("gemm_dma", 1)
+        y1 = kk.linear(x, w, b)
+        s1 = kk.linear_bn_stats(x, w) if Kd % 8 == 0 else None
+    finally:
+        kk.set_tuning("gemm_dma", 0)
+    assert torch.equal(y0, y1)
+    if s0 is not None:
+        for a, c in zip(s0, s1):
+            assert torch.equal(a, c)
+    assert rel_err(y1.float(), x.float() @ w.float().t() + b) < TOL[torch.bfloat16]
