@@ -16,7 +16,7 @@ from ssl_mae_amd import kernels as K  # noqa: E402
 from gemm_ksweep import timeit  # noqa: E402
 
 B = 256
-SHAPES = [  # (name, M, N, K, bias, gelu, stats)
+SHAPES = [  # (name, M, N, K, bias, gelu, stats); "dX": dy [M, K] @ w [K, N]; "dXg": + GELU backward
     ("dec qkv fwd", B * 6272, 1152, 384, True, False, False),
     ("dec fc1+gelu fwd", B * 6272, 1536, 384, True, True, False),
     ("dec fc2 fwd", B * 6272, 384, 1536, True, False, False),
@@ -24,6 +24,9 @@ SHAPES = [  # (name, M, N, K, bias, gelu, stats)
     ("s0 expand+stats", B * 8 * 12544, 384, 96, False, False, True),
     ("s1 qkv fwd", B * 8 * 3136, 576, 192, True, False, False),
     ("s1 fc1+gelu", B * 8 * 3136, 768, 192, True, True, False),
+    ("dec qkv dX", B * 6272, 384, 1152, False, "dX", False),
+    ("dec fc1 dX", B * 6272, 384, 1536, False, "dX", False),
+    ("dec fc2 dX+gelu", B * 6272, 1536, 384, False, "dXg", False),
 ]
 
 
@@ -39,7 +42,14 @@ def main():
         x = torch.randn(M, Kd, device="cuda").to(torch.bfloat16)
         w = (torch.randn(N, Kd, device="cuda") * 0.05).to(torch.bfloat16)
         b = torch.randn(N, device="cuda") if bias else None
-        if stats:
+        if gelu in ("dX", "dXg"):            # dx [M, N] = dy [M, K] @ wt [K, N]
+            wt = (torch.randn(Kd, N, device="cuda") * 0.05).to(torch.bfloat16)
+            if gelu == "dX":
+                fn = lambda: K.linear_dx(x, wt)  # noqa: E731
+            else:
+                pre = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+                fn = lambda: K.linear_dx_gelu(x, wt, pre, 0.1, 5)  # noqa: E731
+        elif stats:
             fn = lambda: K.linear_bn_stats(x, w)  # noqa: E731
         else:
             fn = lambda: K.linear(x, w, b, gelu=gelu)  # noqa: E731

@@ -1012,7 +1012,10 @@ constexpr int DA_BYTES = 256 * DK * 2, DB_BYTES = 128 * DK * 2, DSTAGE = DA_BYTE
 SM_DEV int kmaj32_off(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
 typedef __attribute__((address_space(3))) void lds_void;
 
-template <typename TC, int IMP = 0>
+// BK: B K-major [N][K] (forward) or M/N-major [K][N] (data gradient: a [32][128] image read
+// with ds_read_b64_tr_b16, one 1-KB piece = 4 k-rows x 256 B).  IMP 8: output BatchNorm
+// statistics epilogue; IMP 9: GELU-backward epilogue with the activation side output.
+template <bool BK, typename TC, int IMP = 0>
 __global__ __launch_bounds__(512, 4) void gemm_bf16_dma(GemmArgs g) {
   constexpr int NT = 512, BMV = 256, BNV = 128;
   constexpr int LDS_MAIN = DNS * DSTAGE, LDS_EPI = (NT / 64) * 8192;
@@ -1036,24 +1039,33 @@ __global__ __launch_bounds__(512, 4) void gemm_bf16_dma(GemmArgs g) {
     ca[i] = (l & 3) ^ ((row >> 2) & 3);
     va[i] = m0 + row < g.M ? (uint32_t)(((int64_t)row * g.lda + 8 * ca[i]) * 2) : BUF_OOB;
   }
-  {
+  if constexpr (BK) {
     const int row = 16 * w + (l >> 2);
     cb = (l & 3) ^ ((row >> 2) & 3);
     vb = n0 + row < g.N ? (uint32_t)(((int64_t)row * g.ldb + 8 * cb) * 2) : BUF_OOB;
+  } else {                         // k-row 4w + l / 16, chunk slot l % 16 of its 256-B row
+    const int krow = 4 * w + (l >> 4);
+    cb = krow;                     // (the k tail test uses the k-row)
+    const int c = (l & 15) ^ ((krow & 3) << 2);
+    vb = n0 + 8 * c < g.N ? (uint32_t)(((int64_t)krow * g.ldb + 8 * c) * 2) : BUF_OOB;
   }
-  const int64_t abase = (int64_t)m0 * g.lda, bbase = (int64_t)n0 * g.ldb;
+  const int64_t abase = (int64_t)m0 * g.lda, bbase = BK ? (int64_t)n0 * g.ldb : (int64_t)n0;
   const int nk = ke > kb ? (ke - kb + DK - 1) / DK : 0;
   auto issue = [&](int kt) {
     const int k0 = kb + kt * DK;
     char* st = lds + (kt % DNS) * DSTAGE;
     const auto ra = panel_rsrc(A, abase + k0);
-    const auto rb = panel_rsrc(B, bbase + k0);
+    const auto rb = panel_rsrc(B, bbase + (BK ? (int64_t)k0 : (int64_t)k0 * g.ldb));
 #pragma unroll
     for (int i = 0; i < 2; ++i)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void*)(st + (32 * w + 16 * i) * 64), 16,
                                                k0 + 8 * ca[i] < ke ? va[i] : BUF_OOB, 0, 0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(st + DA_BYTES + 16 * w * 64), 16,
-                                             k0 + 8 * cb < ke ? vb : BUF_OOB, 0, 0, 0);
+    if constexpr (BK)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(st + DA_BYTES + 16 * w * 64), 16,
+                                               k0 + 8 * cb < ke ? vb : BUF_OOB, 0, 0, 0);
+    else
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(st + DA_BYTES + 4 * w * 256), 16,
+                                               k0 + cb < ke ? vb : BUF_OOB, 0, 0, 0);
   };
   f32x16 acc[2][2];
 #pragma unroll
@@ -1082,7 +1094,9 @@ __global__ __launch_bounds__(512, 4) void gemm_bf16_dma(GemmArgs g) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) af[i] = *(const bf16x8*)(la + kmaj32_off(wm + 32 * i + (l & 31), 2 * s + (l >> 5)));
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bfr[j] = *(const bf16x8*)(lb + kmaj32_off(wn + 32 * j + (l & 31), 2 * s + (l >> 5)));
+      for (int j = 0; j < 2; ++j)
+        bfr[j] = BK ? *(const bf16x8*)(lb + kmaj32_off(wn + 32 * j + (l & 31), 2 * s + (l >> 5)))
+                    : lread_frag_r<false, 128>(lb, wn + 32 * j, s);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -1091,7 +1105,7 @@ __global__ __launch_bounds__(512, 4) void gemm_bf16_dma(GemmArgs g) {
     }
   }
   __syncthreads();   // ring dead: the epilogue's row stage reuses it
-  gemm_epilogue<TC, true, 2, 2, IMP == 8, false>(g, acc, m0, n0, wm, wn, l, 0, lds + w * 8192);
+  gemm_epilogue<TC, true, 2, 2, IMP == 8, IMP == 9>(g, acc, m0, n0, wm, wn, l, 0, lds + w * 8192);
 }
 
 // LDS-DMA forward GEMM selection (tuning knob "gemm_dma", sm_set_tuning / SM_GEMM_DMA)
@@ -1258,9 +1272,9 @@ void launch_bf16(const GemmArgs& g, int splits, hipStream_t st) {
   const int v = gemm_variant(g.M, g.N, g.K);
   const int bm = variant_bm(v), bn = variant_bn(v);
   const int tiles = ((g.N + bn - 1) / bn) * ((g.M + bm - 1) / bm);
-  if constexpr (AK && BK && VEC) {
+  if constexpr (AK && VEC) {
     if (v == 2 && splits == 1 && use_dma(g)) {
-      hipLaunchKernelGGL((gemm_bf16_dma<TC>), dim3(tiles), dim3(512), 0, st, g);
+      hipLaunchKernelGGL((gemm_bf16_dma<BK, TC>), dim3(tiles), dim3(512), 0, st, g);
       return;
     }
   }
@@ -1420,7 +1434,8 @@ static int gemm_run(int ab_dtype, int c_dtype, int a_layout, int b_layout, int M
       !((N & 7) || (ldc & 7)) && K > 0) {   // the GELU-backward dX GEMM: IMP 9 epilogue
     const int v = gemm_variant(M, N, K);
     const int tiles = ((N + 127) / 128) * ((M + variant_bm(v) - 1) / variant_bm(v));
-    if (v == 2) hipLaunchKernelGGL((gemm_bf16_v2<true, false, __bf16, true, 256, 9>), dim3(tiles), dim3(512), 0, stream, g);
+    if (v == 2 && use_dma(g)) hipLaunchKernelGGL((gemm_bf16_dma<false, __bf16, 9>), dim3(tiles), dim3(512), 0, stream, g);
+    else if (v == 2) hipLaunchKernelGGL((gemm_bf16_v2<true, false, __bf16, true, 256, 9>), dim3(tiles), dim3(512), 0, stream, g);
     else hipLaunchKernelGGL((gemm_bf16_v2<true, false, __bf16, true, 128, 9>), dim3(tiles), dim3(256), 0, stream, g);
     SM_CHECK_LAUNCH();
     rc = 0;
@@ -1460,7 +1475,8 @@ extern "C" int sm_linear_dx_gelu(int M, int N, int K, const void* dy, const void
   g.drop_p = drop_p; g.seed = seed; g.rows_per_group = 1; g.k_begin = 0; g.k_chunk = N;
   const int v = gemm_variant(g.M, g.N, g.K);
   const int tiles = ((g.N + 127) / 128) * ((g.M + variant_bm(v) - 1) / variant_bm(v));
-  if (v == 2) hipLaunchKernelGGL((gemm_bf16_v2<true, false, __bf16, true, 256, 9>), dim3(tiles), dim3(512), 0, stream, g);
+  if (v == 2 && use_dma(g)) hipLaunchKernelGGL((gemm_bf16_dma<false, __bf16, 9>), dim3(tiles), dim3(512), 0, stream, g);
+  else if (v == 2) hipLaunchKernelGGL((gemm_bf16_v2<true, false, __bf16, true, 256, 9>), dim3(tiles), dim3(512), 0, stream, g);
   else hipLaunchKernelGGL((gemm_bf16_v2<true, false, __bf16, true, 128, 9>), dim3(tiles), dim3(256), 0, stream, g);
   SM_CHECK_LAUNCH();
   return 0;
@@ -1635,7 +1651,7 @@ extern "C" int sm_linear_bn_stats(int M, int N, int K, const void* x, const void
   g.stat_part = part;
   const int tiles_n = (N + 127) / 128;
   if (gemm_variant(M, N, K) == 2 && use_dma(g))
-    hipLaunchKernelGGL((gemm_bf16_dma<__bf16, 8>), dim3(tiles_n * ((M + 255) / 256)), dim3(512), 0, stream, g);
+    hipLaunchKernelGGL((gemm_bf16_dma<true, __bf16, 8>), dim3(tiles_n * ((M + 255) / 256)), dim3(512), 0, stream, g);
   else if (gemm_variant(M, N, K) == 2)
     hipLaunchKernelGGL((gemm_bf16_v2<true, true, __bf16, true, 256, 8>), dim3(tiles_n * ((M + 255) / 256)), dim3(512),
                        0, stream, g);
