@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--only", default="")
+    ap.add_argument("--variants", default="0,1,2", help="gemm_dma knob values: 0 v2, 1 DMA 3-stage, 2 DMA 6-stage")
     args = ap.parse_args()
     for name, M, N, Kd, bias, gelu, stats in SHAPES:
         if args.only and args.only not in name:
@@ -53,20 +54,22 @@ def main():
             fn = lambda: K.linear_bn_stats(x, w)  # noqa: E731
         else:
             fn = lambda: K.linear(x, w, b, gelu=gelu)  # noqa: E731
-        t = {0: [], 1: []}
+        vs = [int(v) for v in args.variants.split(",")]
+        t = {v: [] for v in vs}
         outs = {}
         for _ in range(args.reps):
-            for v in (0, 1):
+            for v in vs:
                 K.set_tuning("gemm_dma", v)
                 t[v].append(timeit(fn, args.iters))
                 o = fn()
                 outs[v] = o[0] if isinstance(o, tuple) else o
         K.set_tuning("gemm_dma", 0)
-        same = torch.equal(outs[0], outs[1])
+        same = all(torch.equal(outs[vs[0]], outs[v]) for v in vs)
         f = 2.0 * M * N * Kd
-        t0, t1 = min(t[0]), min(t[1])
-        print(f"{name:18s} M={M} N={N} K={Kd}: v2 {t0:7.3f} ms ({f / t0 / 1e9:6.0f} TF/s) | dma {t1:7.3f} ms "
-              f"({f / t1 / 1e9:6.0f} TF/s)  {t0 / t1:5.2f}x  bit-identical {same}", flush=True)
+        t0 = min(t[vs[0]])
+        cols = " | ".join(f"knob {v}: {min(t[v]):7.3f} ms ({f / min(t[v]) / 1e9:5.0f} TF/s, {t0 / min(t[v]):4.2f}x)"
+                          for v in vs)
+        print(f"{name:18s} M={M} N={N} K={Kd}: {cols}  bit-identical {same}", flush=True)
         del x, w, b, outs
         torch.cuda.empty_cache()
 

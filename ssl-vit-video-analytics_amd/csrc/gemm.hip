@@ -936,7 +936,7 @@ __global__ __launch_bounds__(BMV * 2, (BMV == 256 && IMP != 5 && IMP != 6 && IMP
           }
           ra[i] = pack8(v, (__bf16*)nullptr);
         }
-      } else {
+      } else if (c0 < ke) {   // chunks past K stay the zeros the loads returned
         // x = bf16(a sc + sh), as bn_apply stores it; one channel pair at a time (few live
         // registers beside the accumulators: the plain kernel's 4 waves / SIMD)
 #pragma unroll
@@ -1007,7 +1007,7 @@ __global__ __launch_bounds__(BMV * 2, (BMV == 256 && IMP != 5 && IMP != 6 && IMP
 // image (conflict-free ds_read_b128 fragments) is produced by choosing which 16-B chunk
 // of its row each lane fetches.  Rows past M / N and chunks past K read zero through an
 // out-of-range voffset.
-constexpr int DK = 32, DNS = 3;
+constexpr int DK = 32;
 constexpr int DA_BYTES = 256 * DK * 2, DB_BYTES = 128 * DK * 2, DSTAGE = DA_BYTES + DB_BYTES;
 SM_DEV int kmaj32_off(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
 typedef __attribute__((address_space(3))) void lds_void;
@@ -1015,8 +1015,8 @@ typedef __attribute__((address_space(3))) void lds_void;
 // BK: B K-major [N][K] (forward) or M/N-major [K][N] (data gradient: a [32][128] image read
 // with ds_read_b64_tr_b16, one 1-KB piece = 4 k-rows x 256 B).  IMP 8: output BatchNorm
 // statistics epilogue; IMP 9: GELU-backward epilogue with the activation side output.
-template <bool BK, typename TC, int IMP = 0>
-__global__ __launch_bounds__(512, 4) void gemm_bf16_dma(GemmArgs g) {
+template <bool BK, typename TC, int IMP = 0, int DNS = 3>
+__global__ __launch_bounds__(512, DNS == 3 ? 4 : 2) void gemm_bf16_dma(GemmArgs g) {
   constexpr int NT = 512, BMV = 256, BNV = 128;
   constexpr int LDS_MAIN = DNS * DSTAGE, LDS_EPI = (NT / 64) * 8192;
   __shared__ __attribute__((aligned(16))) char lds[LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI];
@@ -1074,18 +1074,22 @@ __global__ __launch_bounds__(512, 4) void gemm_bf16_dma(GemmArgs g) {
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  if (nk > 0) issue(0);
-  if (nk > 1) issue(1);
+  for (int kt = 0; kt < DNS - 1 && kt < nk; ++kt) issue(kt);
   for (int kt = 0; kt < nk; ++kt) {
     // this wave's pieces of stage kt have landed (the next stage's 3 may stay in flight);
     // the barrier then publishes every wave's pieces and retires the slot stage kt + 2 reuses
     // (s_barrier without __syncthreads' fence: the fence would wait for every outstanding
     // DMA, the next stage's included)
-    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    // (DNS - 2 later stages may stay in flight: 3 pieces each)
+    const int later = min(nk - 1 - kt, DNS - 2);
+    if (later >= 4) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (later == 3) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+    else if (later == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (later == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (kt + 2 < nk) issue(kt + 2);
+    if (kt + DNS - 1 < nk) issue(kt + DNS - 1);
     const char* la = lds + (kt % DNS) * DSTAGE;
     const char* lb = la + DA_BYTES;
 #pragma unroll
@@ -1274,7 +1278,10 @@ void launch_bf16(const GemmArgs& g, int splits, hipStream_t st) {
   const int tiles = ((g.N + bn - 1) / bn) * ((g.M + bm - 1) / bm);
   if constexpr (AK && VEC) {
     if (v == 2 && splits == 1 && use_dma(g)) {
-      hipLaunchKernelGGL((gemm_bf16_dma<BK, TC>), dim3(tiles), dim3(512), 0, st, g);
+      if (sm_tuning_get(SM_TUNE_GEMM_DMA) == 2)
+        hipLaunchKernelGGL((gemm_bf16_dma<BK, TC, 0, 6>), dim3(tiles), dim3(512), 0, st, g);
+      else
+        hipLaunchKernelGGL((gemm_bf16_dma<BK, TC>), dim3(tiles), dim3(512), 0, st, g);
       return;
     }
   }

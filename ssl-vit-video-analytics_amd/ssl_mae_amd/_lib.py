@@ -64,7 +64,7 @@ _SIGS = {
     "sm_linear_bn_stats": (_c_i32, [_c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_f32,
                                     _c_f32, _c_i32, _c_p, _c_i64, _c_p]),
     "sm_linear_bnin": (_c_i32, [_c_i32, _c_i32, _c_i32] + [_c_p] * 7 + [_c_p]),
-    "sm_linear_bnin_bn_stats": (_c_i32, [_c_i32, _c_i32, _c_i32] + [_c_p] * 11 + [_c_f32, _c_f32, _c_i32, _c_p, _c_i64,
+    "sm_linear_bnin_bn_stats": (_c_i32, [_c_i32, _c_i32, _c_i32] + [_c_p] * 12 + [_c_f32, _c_f32, _c_i32, _c_p, _c_i64,
                                                                                   _c_p]),
     "sm_bn_apply_res_bn": (_c_i32, [_c_i32, _c_i32, _c_i64, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i32, _c_p,
                                     _c_p, _c_p, _c_p, _c_p, _c_p, _c_i64, _c_p]),

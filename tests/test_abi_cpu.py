@@ -67,3 +67,18 @@ def test_torch_library_registration():
         col, geom = ops.stem_im2col(clip, torch.bfloat16)
         assert col.shape == (2 * 8 * 112 * 112, 32) and geom == (16, 112, 112)
         assert ops.patchify(clip).shape == (2, 8 * 28 * 28, 192)
+
+
+def test_binding_argument_counts_match_header():
+    """Every ctypes signature in _lib._SIGS has as many arguments as the header declares
+    (a pointer missing from a binding shifts every later argument)."""
+    from ssl_mae_amd import _lib
+    src = open(os.path.join(ROOT, "include", "sm_api.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    decls = {}
+    for m in re.finditer(r"\b(sm_[a-z0-9_]+)\s*\(([^)]*)\)\s*;", src):
+        params = m.group(2).strip()
+        decls[m.group(1)] = 0 if params in ("", "void") else params.count(",") + 1
+    for name, (_, argtypes) in _lib._SIGS.items():
+        assert name in decls, name
+        assert len(argtypes) == decls[name], (name, len(argtypes), decls[name])
