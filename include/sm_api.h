@@ -113,11 +113,6 @@ int sm_linear_dw_se(int rows, int nout, int nin, const void* dy, const void* a2,
                     const float* act_rstd, const float* act_w, const float* act_b, int act_gelu, const float* gate,
                     int hw, float* dW, int accumulate, void* ws, int64_t ws_bytes, hipStream_t stream);
 
-/* ---- kernel-variant knobs for same-process A/B measurement: "gemm_dma" (0/1: the LDS-DMA
- * ring forward GEMM), "attn_bwd" (attention-backward variant, 0 = default).  Returns 0, or
- * -2 for an unknown name.  Start values from SM_GEMM_DMA / SM_ATTN_BWD_VAR. */
-int sm_set_tuning(const char* name, int value);
-
 /* ---- fused attention (tiny_vit.py:103 F.scaled_dot_product_attention;
  * torch MultiheadAttention core of the decoder, mae_vit_adapter.py:40-48).
  * qkv packed [N][L][3][H][D] bf16|f32, out O [N][L][H][D], lse [N][H][L]. */

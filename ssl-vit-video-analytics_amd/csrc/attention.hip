@@ -450,7 +450,7 @@ __global__ void attn_delta_kernel(AttnArgs a, int D) {
 // Row constants folded in: without dropout the dP accumulator starts at -Delta
 // (dS = P * acc); with it, log2(1/(1-p)) is folded into the LSE so the exp yields
 // P' = P/(1-p) directly (dV needs no final scale) and Delta is stored as Delta(1-p).
-template <int D, bool DROP, int NW = 4, bool PRIO = false>
+template <int D, bool DROP, int NW = 4>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_bf16(AttnArgs a) {
   constexpr int QT = 64;
   constexpr int RB = 32 * D * 2;
@@ -577,9 +577,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_bf16(AttnArgs a
   };
 
   uint4 rq[Stager<D, QT, 64 * NW>::CH], rd[Stager<D, QT, 64 * NW>::CH];
-  // static priority for one wave of each SIMD pair (MI355X_MICROARCH.md item 4): the
-  // younger half of an 8-wave block, or every other 4-wave block
-  if (PRIO && (NW == 8 ? w >= 4 : ((blockIdx.x >> 3) & 1))) __builtin_amdgcn_s_setprio(1);
   // the tile's row constants (LSE, Delta) are prefetched with its Q / dO rows (wave 0,
   // one row per lane, index clamped: no branch); loading them between the two barriers
   // held every wave of the block for a global-load round trip per tile
@@ -636,7 +633,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_bf16(AttnArgs a
 
 // =============================================================== bf16 backward dQ
 // Queries on lanes; K / V tiles staged with prefetch; dQ^T = K^T dS^T.
-template <int D, bool DROP, int NW = 4, bool PRIO = false>
+template <int D, bool DROP, int NW = 4>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_bf16(AttnArgs a) {
   constexpr int KT = 64;
   constexpr int RB = 32 * D * 2;
@@ -706,9 +703,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_bf16(AttnArgs a) 
   uint4 rk[Stager<D, KT, 64 * NW>::CH], rv[Stager<D, KT, 64 * NW>::CH];
   stg.load(kb, a.L, rk);
   stg.load(vb, a.L, rv);
-  // static priority for one wave of each SIMD pair (MI355X_MICROARCH.md item 4): the
-  // younger half of an 8-wave block, or every other 4-wave block
-  if (PRIO && (NW == 8 ? w >= 4 : ((blockIdx.x >> 3) & 1))) __builtin_amdgcn_s_setprio(1);
   // one key tile; the ragged last tile is its own instantiation (see the forward)
   auto tile = [&](int k0, auto rag) {
     constexpr bool RAGGED = decltype(rag)::value;
@@ -913,28 +907,12 @@ __global__ __launch_bounds__(128) void attn_bwd_dkdv_f32(AttnArgs a) {
 }
 
 // dQ first: it forms Delta = rowsum(dO*O) in its prologue for the dK/dV kernel
+// dQ first: it forms Delta = rowsum(dO*O) in its prologue and writes bf16(Q scale log2 e)
+// for the dK/dV kernel.  (8-wave blocks and a static s_setprio for one wave of each SIMD
+// pair measured 1-10 % slower, profiles/r04c_attn_bwd_variants.txt.)
 template <int D, bool DROP>
-void launch_attn_bwd(const AttnArgs& a, int var, hipStream_t st) {
-  const unsigned nh = (unsigned)(a.H * a.N);
-  const dim3 g4((unsigned)((a.L + 127) / 128) * nh), g8((unsigned)((a.L + 255) / 256) * nh);
-  if constexpr (D == 64) {
-    if (var == 1 || var == 2) {
-      hipLaunchKernelGGL((attn_bwd_dq_bf16<D, DROP>), g4, dim3(256), 0, st, a);
-      if (var == 1) hipLaunchKernelGGL((attn_bwd_dkdv_bf16<D, DROP, 8>), g8, dim3(512), 0, st, a);
-      else hipLaunchKernelGGL((attn_bwd_dkdv_bf16<D, DROP, 8, true>), g8, dim3(512), 0, st, a);
-      return;
-    }
-    if (var == 3) {
-      hipLaunchKernelGGL((attn_bwd_dq_bf16<D, DROP, 4, true>), g4, dim3(256), 0, st, a);
-      hipLaunchKernelGGL((attn_bwd_dkdv_bf16<D, DROP, 4, true>), g4, dim3(256), 0, st, a);
-      return;
-    }
-    if (var == 4) {
-      hipLaunchKernelGGL((attn_bwd_dq_bf16<D, DROP, 8, true>), g8, dim3(512), 0, st, a);
-      hipLaunchKernelGGL((attn_bwd_dkdv_bf16<D, DROP, 8, true>), g8, dim3(512), 0, st, a);
-      return;
-    }
-  }
+void launch_attn_bwd(const AttnArgs& a, hipStream_t st) {
+  const dim3 g4((unsigned)((a.L + 127) / 128) * (unsigned)(a.H * a.N));
   hipLaunchKernelGGL((attn_bwd_dq_bf16<D, DROP>), g4, dim3(256), 0, st, a);
   hipLaunchKernelGGL((attn_bwd_dkdv_bf16<D, DROP>), g4, dim3(256), 0, st, a);
 }
@@ -988,9 +966,8 @@ extern "C" int sm_attn_bwd(int dtype, int N, int L, int H, int D, const void* qk
   const bool drop = drop_p > 0.f;
   if (dtype == SM_BF16) {
     // dQ first: it forms Delta = rowsum(dO*O) in its prologue for the dK/dV kernel
-    const int var = sm_tuning_get(SM_TUNE_ATTN_BWD);
-    if (D == 32) { if (drop) launch_attn_bwd<32, true>(a, var, st); else launch_attn_bwd<32, false>(a, var, st); }
-    else { if (drop) launch_attn_bwd<64, true>(a, var, st); else launch_attn_bwd<64, false>(a, var, st); }
+    if (D == 32) { if (drop) launch_attn_bwd<32, true>(a, st); else launch_attn_bwd<32, false>(a, st); }
+    else { if (drop) launch_attn_bwd<64, true>(a, st); else launch_attn_bwd<64, false>(a, st); }
   } else {
     const int dblocks = (int)(((int64_t)N * L + 3) / 4);
     hipLaunchKernelGGL(attn_delta_kernel<float>, dim3(dblocks), dim3(256), 0, st, a, D);

@@ -257,10 +257,5 @@ static inline void colred(const float* part, int nb, int ncols, double* outd, fl
                      accumulate);
 }
 
-// Kernel-variant knobs for same-process A/B measurements (sm_set_tuning in mae.hip; the
-// environment variables SM_GEMM_DMA / SM_ATTN_BWD_VAR give the start values).
-enum SmTune { SM_TUNE_GEMM_DMA = 0, SM_TUNE_ATTN_BWD = 1, SM_TUNE_COUNT = 4 };
-int sm_tuning_get(int knob);
-
 #define SM_CHECK_LAUNCH() \
   do { hipError_t e__ = hipGetLastError(); if (e__ != hipSuccess) return (int)e__; } while (0)

@@ -460,6 +460,10 @@ SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x
   }
 }
 
+// (Round 4: an LDS-DMA ring form of the v2 kernel -- buffer_load ... lds into a 3- or 6-slot
+// ring of 32-K stages, no staging registers or ds_write, one barrier per stage -- gave
+// bit-identical outputs 4-40 % slower on every K-major forward and data-gradient shape of
+// the step, profiles/r04d_gemm_dma_ab_and_ksweep.txt; removed.)
 // One 128x128 output tile per block; 1-D grid over (m-tile, n-tile) with an
 // XCD-aware bijective remap: the n-tiles of one m-tile (which share the A panel)
 // are dispatched to the same XCD's L2.  (A persistent variant that prefetched the
@@ -998,125 +1002,6 @@ __global__ __launch_bounds__(BMV * 2, (BMV == 256 && IMP != 5 && IMP != 6 && IMP
                                                                           lds + w * 8192);
 }
 
-// ============================================================ bf16 MFMA kernel, LDS-DMA ring
-// K-major A and B (every Linear / 1x1-conv forward).  256 x 128 block tile on 8 waves of
-// 64 x 64 (as v2, same epilogue), K staged DK = 32 at a time through a DNS = 3-slot LDS ring
-// filled by buffer_load ... lds (LDS-DMA: no staging registers and no ds_write), one
-// barrier per stage, two stages in flight while one is consumed.  Each 1-KB DMA piece
-// covers 16 tile rows x 64 B; lane l lands at piece + 16 l, so the XOR swizzle of the
-// image (conflict-free ds_read_b128 fragments) is produced by choosing which 16-B chunk
-// of its row each lane fetches.  Rows past M / N and chunks past K read zero through an
-// out-of-range voffset.
-constexpr int DK = 32;
-constexpr int DA_BYTES = 256 * DK * 2, DB_BYTES = 128 * DK * 2, DSTAGE = DA_BYTES + DB_BYTES;
-SM_DEV int kmaj32_off(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
-typedef __attribute__((address_space(3))) void lds_void;
-
-// BK: B K-major [N][K] (forward) or M/N-major [K][N] (data gradient: a [32][128] image read
-// with ds_read_b64_tr_b16, one 1-KB piece = 4 k-rows x 256 B).  IMP 8: output BatchNorm
-// statistics epilogue; IMP 9: GELU-backward epilogue with the activation side output.
-template <bool BK, typename TC, int IMP = 0, int DNS = 3>
-__global__ __launch_bounds__(512, DNS == 3 ? 4 : 2) void gemm_bf16_dma(GemmArgs g) {
-  constexpr int NT = 512, BMV = 256, BNV = 128;
-  constexpr int LDS_MAIN = DNS * DSTAGE, LDS_EPI = (NT / 64) * 8192;
-  __shared__ __attribute__((aligned(16))) char lds[LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI];
-  const int ntn = (g.N + BNV - 1) / BNV;
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int m0 = (tile / ntn) * BMV, n0 = (tile % ntn) * BNV;
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
-  const __bf16* A = (const __bf16*)g.A;
-  const __bf16* B = (const __bf16*)g.B;
-  const int kb = g.k_begin, ke = min(g.K, kb + g.k_chunk);
-  // DMA plan: wave w fills A rows [32w, 32w + 32) (two pieces) and B rows [16w, 16w + 16)
-  uint32_t va[2], vb;
-  int ca[2], cb;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = 32 * w + 16 * i + (l >> 2);
-    ca[i] = (l & 3) ^ ((row >> 2) & 3);
-    va[i] = m0 + row < g.M ? (uint32_t)(((int64_t)row * g.lda + 8 * ca[i]) * 2) : BUF_OOB;
-  }
-  if constexpr (BK) {
-    const int row = 16 * w + (l >> 2);
-    cb = (l & 3) ^ ((row >> 2) & 3);
-    vb = n0 + row < g.N ? (uint32_t)(((int64_t)row * g.ldb + 8 * cb) * 2) : BUF_OOB;
-  } else {                         // k-row 4w + l / 16, chunk slot l % 16 of its 256-B row
-    const int krow = 4 * w + (l >> 4);
-    cb = krow;                     // (the k tail test uses the k-row)
-    const int c = (l & 15) ^ ((krow & 3) << 2);
-    vb = n0 + 8 * c < g.N ? (uint32_t)(((int64_t)krow * g.ldb + 8 * c) * 2) : BUF_OOB;
-  }
-  const int64_t abase = (int64_t)m0 * g.lda, bbase = BK ? (int64_t)n0 * g.ldb : (int64_t)n0;
-  const int nk = ke > kb ? (ke - kb + DK - 1) / DK : 0;
-  auto issue = [&](int kt) {
-    const int k0 = kb + kt * DK;
-    char* st = lds + (kt % DNS) * DSTAGE;
-    const auto ra = panel_rsrc(A, abase + k0);
-    const auto rb = panel_rsrc(B, bbase + (BK ? (int64_t)k0 : (int64_t)k0 * g.ldb));
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void*)(st + (32 * w + 16 * i) * 64), 16,
-                                               k0 + 8 * ca[i] < ke ? va[i] : BUF_OOB, 0, 0, 0);
-    if constexpr (BK)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(st + DA_BYTES + 16 * w * 64), 16,
-                                               k0 + 8 * cb < ke ? vb : BUF_OOB, 0, 0, 0);
-    else
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(st + DA_BYTES + 4 * w * 256), 16,
-                                               k0 + cb < ke ? vb : BUF_OOB, 0, 0, 0);
-  };
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  for (int kt = 0; kt < DNS - 1 && kt < nk; ++kt) issue(kt);
-  for (int kt = 0; kt < nk; ++kt) {
-    // this wave's pieces of stage kt have landed (the next stage's 3 may stay in flight);
-    // the barrier then publishes every wave's pieces and retires the slot stage kt + 2 reuses
-    // (s_barrier without __syncthreads' fence: the fence would wait for every outstanding
-    // DMA, the next stage's included)
-    // (DNS - 2 later stages may stay in flight: 3 pieces each)
-    const int later = min(nk - 1 - kt, DNS - 2);
-    if (later >= 4) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    else if (later == 3) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-    else if (later == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else if (later == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (kt + DNS - 1 < nk) issue(kt + DNS - 1);
-    const char* la = lds + (kt % DNS) * DSTAGE;
-    const char* lb = la + DA_BYTES;
-#pragma unroll
-    for (int s = 0; s < DK / 16; ++s) {
-      bf16x8 af[2], bfr[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = *(const bf16x8*)(la + kmaj32_off(wm + 32 * i + (l & 31), 2 * s + (l >> 5)));
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        bfr[j] = BK ? *(const bf16x8*)(lb + kmaj32_off(wn + 32 * j + (l & 31), 2 * s + (l >> 5)))
-                    : lread_frag_r<false, 128>(lb, wn + 32 * j, s);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-    }
-  }
-  __syncthreads();   // ring dead: the epilogue's row stage reuses it
-  gemm_epilogue<TC, true, 2, 2, IMP == 8, IMP == 9>(g, acc, m0, n0, wm, wn, l, 0, lds + w * 8192);
-}
-
-// LDS-DMA forward GEMM selection (tuning knob "gemm_dma", sm_set_tuning / SM_GEMM_DMA)
-bool use_dma(const GemmArgs& g) {
-  return sm_tuning_get(SM_TUNE_GEMM_DMA) && g.partial == nullptr && g.M >= 192;
-}
-
 // ============================================================ f32 MFMA kernel
 constexpr int FBM = 64, FBN = 64, FBK = 16, FLD = 64 + 4;
 
@@ -1276,15 +1161,6 @@ void launch_bf16(const GemmArgs& g, int splits, hipStream_t st) {
   const int v = gemm_variant(g.M, g.N, g.K);
   const int bm = variant_bm(v), bn = variant_bn(v);
   const int tiles = ((g.N + bn - 1) / bn) * ((g.M + bm - 1) / bm);
-  if constexpr (AK && VEC) {
-    if (v == 2 && splits == 1 && use_dma(g)) {
-      if (sm_tuning_get(SM_TUNE_GEMM_DMA) == 2)
-        hipLaunchKernelGGL((gemm_bf16_dma<BK, TC, 0, 6>), dim3(tiles), dim3(512), 0, st, g);
-      else
-        hipLaunchKernelGGL((gemm_bf16_dma<BK, TC>), dim3(tiles), dim3(512), 0, st, g);
-      return;
-    }
-  }
   if (v == 1) hipLaunchKernelGGL((gemm_bf16_kernel<AK, BK, TC, VEC>), dim3(tiles, 1, splits), dim3(256), 0, st, g);
   else if (v == 2) hipLaunchKernelGGL((gemm_bf16_v2<AK, BK, TC, VEC, 256>), dim3(tiles * splits), dim3(512), 0, st, g);
   else hipLaunchKernelGGL((gemm_bf16_v2<AK, BK, TC, VEC, 128>), dim3(tiles * splits), dim3(256), 0, st, g);
@@ -1441,8 +1317,7 @@ static int gemm_run(int ab_dtype, int c_dtype, int a_layout, int b_layout, int M
       !((N & 7) || (ldc & 7)) && K > 0) {   // the GELU-backward dX GEMM: IMP 9 epilogue
     const int v = gemm_variant(M, N, K);
     const int tiles = ((N + 127) / 128) * ((M + variant_bm(v) - 1) / variant_bm(v));
-    if (v == 2 && use_dma(g)) hipLaunchKernelGGL((gemm_bf16_dma<false, __bf16, 9>), dim3(tiles), dim3(512), 0, stream, g);
-    else if (v == 2) hipLaunchKernelGGL((gemm_bf16_v2<true, false, __bf16, true, 256, 9>), dim3(tiles), dim3(512), 0, stream, g);
+    if (v == 2) hipLaunchKernelGGL((gemm_bf16_v2<true, false, __bf16, true, 256, 9>), dim3(tiles), dim3(512), 0, stream, g);
     else hipLaunchKernelGGL((gemm_bf16_v2<true, false, __bf16, true, 128, 9>), dim3(tiles), dim3(256), 0, stream, g);
     SM_CHECK_LAUNCH();
     rc = 0;
@@ -1482,8 +1357,7 @@ extern "C" int sm_linear_dx_gelu(int M, int N, int K, const void* dy, const void
   g.drop_p = drop_p; g.seed = seed; g.rows_per_group = 1; g.k_begin = 0; g.k_chunk = N;
   const int v = gemm_variant(g.M, g.N, g.K);
   const int tiles = ((g.N + 127) / 128) * ((g.M + variant_bm(v) - 1) / variant_bm(v));
-  if (v == 2 && use_dma(g)) hipLaunchKernelGGL((gemm_bf16_dma<false, __bf16, 9>), dim3(tiles), dim3(512), 0, stream, g);
-  else if (v == 2) hipLaunchKernelGGL((gemm_bf16_v2<true, false, __bf16, true, 256, 9>), dim3(tiles), dim3(512), 0, stream, g);
+  if (v == 2) hipLaunchKernelGGL((gemm_bf16_v2<true, false, __bf16, true, 256, 9>), dim3(tiles), dim3(512), 0, stream, g);
   else hipLaunchKernelGGL((gemm_bf16_v2<true, false, __bf16, true, 128, 9>), dim3(tiles), dim3(256), 0, stream, g);
   SM_CHECK_LAUNCH();
   return 0;
@@ -1657,9 +1531,7 @@ extern "C" int sm_linear_bn_stats(int M, int N, int K, const void* x, const void
   g.alpha = 1.f; g.beta = 0.f; g.rows_per_group = 1; g.k_begin = 0; g.k_chunk = K;
   g.stat_part = part;
   const int tiles_n = (N + 127) / 128;
-  if (gemm_variant(M, N, K) == 2 && use_dma(g))
-    hipLaunchKernelGGL((gemm_bf16_dma<true, __bf16, 8>), dim3(tiles_n * ((M + 255) / 256)), dim3(512), 0, stream, g);
-  else if (gemm_variant(M, N, K) == 2)
+  if (gemm_variant(M, N, K) == 2)
     hipLaunchKernelGGL((gemm_bf16_v2<true, true, __bf16, true, 256, 8>), dim3(tiles_n * ((M + 255) / 256)), dim3(512),
                        0, stream, g);
   else

@@ -14,8 +14,6 @@
 //    a GradScaler-style non-finite check (step skipped on inf/nan, no host sync),
 //    refreshing the bf16 weight shadow in the same pass.
 #include "common.h"
-#include <stdlib.h>
-#include <string.h>
 #include "sm_api.h"
 
 namespace {
@@ -334,30 +332,6 @@ inline int ew_blocks(int64_t n) {
 }
 
 }  // namespace
-
-// ---- kernel-variant knobs (common.h SmTune)
-static int g_tune[SM_TUNE_COUNT];
-static bool g_tune_init = false;
-static void tune_init() {
-  if (g_tune_init) return;
-  const char* e = getenv("SM_GEMM_DMA");
-  g_tune[SM_TUNE_GEMM_DMA] = e ? atoi(e) : 0;
-  e = getenv("SM_ATTN_BWD_VAR");
-  g_tune[SM_TUNE_ATTN_BWD] = e ? atoi(e) : 0;
-  g_tune_init = true;
-}
-int sm_tuning_get(int knob) {
-  tune_init();
-  return knob >= 0 && knob < SM_TUNE_COUNT ? g_tune[knob] : 0;
-}
-extern "C" int sm_set_tuning(const char* name, int value) {
-  tune_init();
-  if (!name) return -2;
-  if (!strcmp(name, "gemm_dma")) g_tune[SM_TUNE_GEMM_DMA] = value;
-  else if (!strcmp(name, "attn_bwd")) g_tune[SM_TUNE_ATTN_BWD] = value;
-  else return -2;
-  return 0;
-}
 
 #define DISPATCH1(DT, ...)                                       \
   do {                                                         \

@@ -28,7 +28,6 @@ _SIGS = {
                          _c_p, _c_i64, _c_p]),
     "sm_attn_fwd": (_c_i32, [_c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_f32, _c_f32, _c_u64,
                              _c_p]),
-    "sm_set_tuning": (_c_i32, [ctypes.c_char_p, _c_i32]),
     "sm_attn_bwd_workspace_bytes": (_c_i64, [_c_i32] * 5),
     "sm_attn_bwd": (_c_i32, [_c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_f32,
                              _c_f32, _c_u64, _c_p]),

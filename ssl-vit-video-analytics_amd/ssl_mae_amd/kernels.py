@@ -211,11 +211,6 @@ def colsum(x, out, accumulate=True):
     return out
 
 
-def set_tuning(name, value):
-    """Select a kernel variant for A/B measurement (sm_set_tuning): 'gemm_dma', 'attn_bwd'."""
-    call("sm_set_tuning", name.encode(), int(value))
-
-
 # ------------------------------------------------------------------ attention
 def attn_fwd(qkv, N, L, H, D, drop_p=0.0, seed=0):
     _chk(qkv)
