@@ -1,0 +1,160 @@
+"""The timed bf16 path pinned per stage and per parameter (SURVEY.md §8(a)
+rows A5-A16, reference src/train_ssl_mae.py:66-91, src/models/tiny_vit.py:166-176,
+src/models/mae_vit_adapter.py:75-117).
+
+The fp32 parity mode runs exact-fp32 kernels and is pinned to 1e-3 of the reference's own
+fp32 steps (tests/test_model_gpu.py).  The benchmarked bf16 kernels are pinned here:
+
+  1. stage by stage at the C2 clip shape (B=1, T=8, 224^2, the golden step's clip and
+     mask): the bf16 model's stem output, stage 0/1/2 outputs and pred against the fp32
+     CPU oracle's (itself checked against the reference's golden activation sums), by
+     relative L2 error (||a - b|| / ||b||) and relative max error (max|a - b| / max|b|).
+     Tolerances, 2x the measured errors (profiles/r04d_bf16_pin_probe.txt: 5.0e-3, 8.9e-3,
+     1.4e-2, 1.9e-2, 1.2e-2 rel L2):
+        stem 1e-2 | stage0 2e-2 | stage1 3e-2 | stage2 4e-2 | pred 3e-2   (rel L2)
+        stem 1.5e-2 | stage0 2e-2 | stage1 3e-2 | stage2 4e-2 | pred 5e-2 (rel max)
+  2. a whole bf16 training step at B=32, T=8, 224^2 (dropout and DropPath ON: both modes
+     draw the same counter-hash masks) against the fp32-mode HIP step on the same clips and
+     mask: loss within 0.1 % (measured 1e-4 at B=16), every parameter gradient with
+     cosine > 0.98 and norm within 5 %, 95 % of them with cosine > 0.995, and the
+     concatenated gradient cosine > 0.999.  Gradients that are zero analytically (biases
+     whose output only feeds a train-mode BatchNorm, e.g. the stem BN2 bias) are skipped:
+     their fp32 norm is rounding noise (< 1e-5 of the largest).
+"""
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+STAGE_TOL = {"act_stem": (1e-2, 1.5e-2), "act_stage0": (2e-2, 2e-2), "act_stage1": (3e-2, 3e-2),
+             "act_stage2": (4e-2, 4e-2), "pred": (3e-2, 5e-2)}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from ssl_mae_amd import _lib
+    _lib.load()
+
+
+def _cfg(B, T, S):
+    return {"dataset": {"clip_len": T, "image_size": S, "stride": 4, "train_split": "-"},
+            "model": {"decoder_embed_dim": 384, "decoder_depth": 4, "decoder_num_heads": 6},
+            "ssl": {"mask_ratio": 0.75, "norm_pix_loss": True},
+            "training": {"batch_size": B, "lr": 5e-4, "log_interval": 20}}
+
+
+def _model(cfg, parity):
+    from ssl_mae_amd import parity_mode
+    from ssl_mae_amd.init_rule import apply_rule
+    from ssl_mae_amd.mae_vit_adapter import TinyVideoMAE
+    from ssl_mae_amd.tiny_vit import tiny_vit_21m_variant
+    torch.manual_seed(42)
+    m = TinyVideoMAE(tiny_vit_21m_variant(img_size=cfg["dataset"]["image_size"]), cfg)
+    apply_rule(m)
+    if parity:
+        parity_mode(m)
+    return m.to(DEV).train()
+
+
+def _errs(a, b):
+    a, b = a.double().cpu().reshape(-1), b.double().cpu().reshape(-1)
+    return ((a - b).norm() / (b.norm() + 1e-30)).item(), ((a - b).abs().max() / (b.abs().max() + 1e-30)).item()
+
+
+def test_bf16_stage_outputs_vs_oracle_c2_clip(golden_dir):
+    from oracle import mae_oracle as O
+    from ssl_mae_amd import kernels as K
+    from ssl_mae_amd import tiny_vit as TV
+    from ssl_mae_amd.init_rule import param_value, synthetic_clip
+    d = np.load(os.path.join(golden_dir, "step_b1_t8_s224.npz"))
+    B, T, S = int(d["B"]), int(d["T"]), int(d["S"])
+    cfg = _cfg(B, T, S)
+    model = _model(cfg, parity=True)
+    clip = torch.from_numpy(synthetic_clip(B, T, S, seed=int(d["clip_seed"]))).to(DEV)
+    mask = torch.from_numpy(d["mask"][0]).bool().to(DEV)
+    for i, st in enumerate(model.encoder.stages):
+        st._pin_stage = i
+    ours = {}
+    pe_run, st_run = TV.PatchEmbed.run, TV._Stage.run
+
+    def pe(self, x, mode):
+        t, xbn = pe_run(self, x, mode)
+        if "act_stem" not in ours:   # the stem output y = BN2(a2) (formed here when BN2 is folded)
+            y = t if xbn is None else K.bn_apply(t.reshape(-1, t.shape[-1]), *xbn[:4], gelu=False).view(t.shape)
+            ours["act_stem"] = y.detach().float().permute(0, 3, 1, 2).cpu()
+        return t, xbn
+
+    def st(self, x, mode, resident=False, x_bn=None):
+        out = st_run(self, x, mode, resident, x_bn)
+        ours.setdefault(f"act_stage{self._pin_stage}", out.detach().float().permute(0, 3, 1, 2).cpu())
+        return out
+    TV.PatchEmbed.run, TV._Stage.run = pe, st
+    try:
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            pred = model(clip, mask)
+    finally:
+        TV.PatchEmbed.run, TV._Stage.run = pe_run, st_run
+    ours["pred"] = pred.detach().float().cpu()
+    P = O.make_params(cfg, param_value)
+    acts = {}
+    with torch.no_grad():
+        O.mae_forward(P, clip.cpu(), mask.cpu(), cfg, None, acts)
+    for k, (tl2, tmax) in STAGE_TOL.items():
+        ref = acts[k].float()
+        if k + "_sumsq" in d.files:   # the oracle run is the reference's (golden activation sums)
+            assert abs(float((ref.double() ** 2).sum()) / float(d[k + "_sumsq"]) - 1) < 1e-4, k
+        l2, mx = _errs(ours[k], ref)
+        assert l2 < tl2 and mx < tmax, (k, l2, mx)
+
+
+def _step(model, clip, bf16):
+    from ssl_mae_amd.optim import FusedAdamW, GradScaler
+    from ssl_mae_amd.train_ssl_mae import train_step
+    opt = FusedAdamW(model.parameters(), lr=5e-4, weight_decay=0.05)
+    torch.manual_seed(42)                 # the same tube mask for both modes
+    loss, pred, idx = train_step(model, clip, opt, GradScaler(), {"mask_ratio": 0.75, "norm_pix_loss": True},
+                                 bf16=bf16)
+    grads = {n: p._sm_grad.detach().double().cpu().clone() for n, p in model.named_parameters()
+             if getattr(p, "_sm_grad", None) is not None and ".stages.3." not in n}
+    return loss.item(), grads
+
+
+def test_bf16_step_vs_fp32_hip_step_b32():
+    from ssl_mae_amd.init_rule import synthetic_clip
+    B, T, S = 32, 8, 224
+    cfg = _cfg(B, T, S)
+    clip = torch.from_numpy(synthetic_clip(B, T, S, seed=77)).to(DEV)
+    res = {}
+    for bf16 in (False, True):
+        model = _model(cfg, parity=False)          # dropout / DropPath on, same masks in both modes
+        res[bf16] = _step(model, clip, bf16)
+        del model
+        torch.cuda.empty_cache()
+    (lf, gf), (lb, gb) = res[False], res[True]
+    assert abs(lb - lf) < 1e-3 * abs(lf), (lb, lf)
+    biggest = max(g.norm().item() for g in gf.values())
+    n_tight, n = 0, 0
+    dot = nf2 = nb2 = 0.0
+    for name, g in gf.items():
+        h = gb[name]
+        nf = g.norm().item()
+        if nf < 1e-5 * biggest:                    # analytically zero (BatchNorm-fed bias)
+            continue
+        cos = float(torch.dot(g.reshape(-1), h.reshape(-1)) / (nf * h.norm().item() + 1e-30))
+        assert cos > 0.98, (name, cos)
+        assert abs(h.norm().item() / nf - 1) < 0.05, name
+        n += 1
+        n_tight += cos > 0.995
+        dot += float(torch.dot(g.reshape(-1), h.reshape(-1)))
+        nf2 += nf * nf
+        nb2 += h.norm().item() ** 2
+    assert n > 190
+    assert n_tight >= 0.95 * n, (n_tight, n)
+    assert dot / math.sqrt(nf2 * nb2) > 0.999
