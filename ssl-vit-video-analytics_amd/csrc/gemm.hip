@@ -171,7 +171,7 @@ struct RowStage {
   // statistics of the output
   template <typename TC, bool STATS = false>
   SM_DEV void flush(int region, TC* out, int64_t ld, int64_t row0, int col0, int M, int N, int l,
-                    float* st1 = nullptr, float* st2 = nullptr) const {
+                    float* st1 = nullptr, float* st2 = nullptr, int wcols = 128 / (int)sizeof(TC)) const {
     constexpr int cpc = 16 / sizeof(TC);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const int c = l & 7;
@@ -186,7 +186,7 @@ struct RowStage {
       const uint4 v = *(const uint4*)(base + region * 4096 + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
       const int64_t row = row0 + r;
       const int col = col0 + c * cpc;
-      if (row < M && col < N) {
+      if (row < M && col < N && c * cpc < wcols) {   // wcols: the wave's own columns of the image
         *(uint4*)(out + row * ld + col) = v;
         if constexpr (STATS) {
           const bf16x8 b = __builtin_bit_cast(bf16x8, v);
@@ -440,10 +440,10 @@ SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x
     if (stage && sizeof(TC) == 2) {     // bf16: one 64-column (128-B) image per i
       const int64_t r0 = m0 + wm + 32 * i;
       const int c0 = n0 + wn;
-      if (g.aux && (g.epi & 1)) rs_.flush<TC>(1, (TC*)g.aux, g.ldc, r0, c0, g.M, g.N, l);
+      if (g.aux && (g.epi & 1)) rs_.flush<TC>(1, (TC*)g.aux, g.ldc, r0, c0, g.M, g.N, l, nullptr, nullptr, 32 * NJ);
       if (AUXS && g.aux_out) rs_.flush<TC>(1, (TC*)g.aux_out, g.ldc, r0, c0, g.M, g.N, l);
       if constexpr (STATS) rs_.flush<TC, true>(0, (TC*)g.C, g.ldc, r0, c0, g.M, g.N, l, st1, st2);
-      else rs_.flush<TC>(0, (TC*)g.C, g.ldc, r0, c0, g.M, g.N, l);
+      else rs_.flush<TC>(0, (TC*)g.C, g.ldc, r0, c0, g.M, g.N, l, nullptr, nullptr, 32 * NJ);
     }
   }
   if (STATS && stage && sizeof(TC) == 2 && l < 8 && m0 + wm < g.M) {   // this wave's 64 rows x 64 cols
@@ -816,9 +816,13 @@ struct XformColsB {
 // SE output formed on load (below).
 // (IMP 5: the activation's registers do not fit beside the staging set at 4 waves /
 // SIMD -- scratch spills inside the K loop -- so it runs at 2 waves / SIMD.)
-template <bool AK, bool BK, typename TC, bool VEC, int BMV, int IMP = 0>
+// BNV: block columns, 128 (waves 64 wide) or 64 (waves 32 wide: narrow outputs such as the
+// stem conv's 48-channel data gradient, where a 128-column tile computed 62.5 % padding).
+template <bool AK, bool BK, typename TC, bool VEC, int BMV, int IMP = 0, int BNV = 128>
 __global__ __launch_bounds__(BMV * 2, (BMV == 256 && IMP != 5 && IMP != 6 && IMP != 7) ? 4 : 2) void gemm_bf16_v2(GemmArgs g) {
-  constexpr int NT = BMV * 2, BNV = 128;
+  constexpr int NT = BMV * 2, NJ = BNV / 64;
+  static_assert(BNV == 128 || (BNV == 64 && IMP != 8 && IMP != 9 && IMP != 10 && IMP != 11),
+                "64-column tiles: no statistics / side-output epilogue");
   constexpr bool XB = IMP == 5 || IMP == 7;
   // A (K-major) formed on load: IMP 6 act(x) * gate (SE output); IMP 11 / 12 a BatchNorm
   // output x = bf16(a sc + sh) from its stored input a (11: plus the IMP 8 statistics)
@@ -844,7 +848,7 @@ __global__ __launch_bounds__(BMV * 2, (BMV == 256 && IMP != 5 && IMP != 6 && IMP
   const int zs = idx / ntiles, tile = idx - zs * ntiles;
   const int m0 = (tile / ntn) * BMV, n0 = (tile % ntn) * BNV;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
+  const int wm = (w >> 1) * 64, wn = (w & 1) * (BNV / 2);
   const __bf16* A = (const __bf16*)g.A;
   const __bf16* B = (const __bf16*)g.B;
   const int kb = g.k_begin + zs * g.k_chunk;
@@ -888,11 +892,11 @@ __global__ __launch_bounds__(BMV * 2, (BMV == 256 && IMP != 5 && IMP != 6 && IMP
     else tlb.load(panel_rsrc(B, bbase + k0 * bstep), ke - k0, r);
   };
 
-  f32x16 acc[2][2];
+  f32x16 acc[2][NJ];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
@@ -971,15 +975,15 @@ __global__ __launch_bounds__(BMV * 2, (BMV == 256 && IMP != 5 && IMP != 6 && IMP
     }
 #pragma unroll
     for (int s = 0; s < BKT / 16; ++s) {
-      bf16x8 af[2], bfr[2];
+      bf16x8 af[2], bfr[NJ];
 #pragma unroll
       for (int i = 0; i < 2; ++i) af[i] = lread_frag_r<AK, BMV>(la, wm + 32 * i, s);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bfr[j] = lread_frag_r<BK, BNV>(lb, wn + 32 * j, s);
+      for (int j = 0; j < NJ; ++j) bfr[j] = lread_frag_r<BK, BNV>(lb, wn + 32 * j, s);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < NJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
     __syncthreads();
@@ -998,8 +1002,8 @@ __global__ __launch_bounds__(BMV * 2, (BMV == 256 && IMP != 5 && IMP != 6 && IMP
     }
     __syncthreads();
   }
-  gemm_epilogue<TC, VEC, 2, 2, IMP == 8 || IMP == 10 || IMP == 11, IMP == 9>(g, acc, m0, n0, wm, wn, l, zs,
-                                                                          lds + w * 8192);
+  gemm_epilogue<TC, VEC, 2, NJ, IMP == 8 || IMP == 10 || IMP == 11, IMP == 9>(g, acc, m0, n0, wm, wn, l, zs,
+                                                                           lds + w * 8192);
 }
 
 // ============================================================ f32 MFMA kernel
@@ -1193,8 +1197,15 @@ template <int IMP, typename TC>
 void launch_conv(const GemmArgs& g, int splits, hipStream_t st) {
   const int v = gemm_variant(g.M, g.N, 0) == 2 ? 2 : 3;
   const int bm = variant_bm(v);
-  dim3 grid(((g.N + 127) / 128) * ((g.M + bm - 1) / bm) * splits);
   constexpr bool AK = IMP == 1 || IMP == 10, BK = AK;
+  if constexpr (IMP == 1) {
+    if (g.N <= 64 && v == 2) {   // narrow output (the stem's 48-channel data gradient): 64-column tiles
+      const dim3 grid(((g.N + 63) / 64) * ((g.M + 255) / 256) * splits);
+      hipLaunchKernelGGL((gemm_bf16_v2<AK, BK, TC, true, 256, IMP, 64>), grid, dim3(512), 0, st, g);
+      return;
+    }
+  }
+  dim3 grid(((g.N + 127) / 128) * ((g.M + bm - 1) / bm) * splits);
   if (v == 2) hipLaunchKernelGGL((gemm_bf16_v2<AK, BK, TC, true, 256, IMP>), grid, dim3(512), 0, st, g);
   else hipLaunchKernelGGL((gemm_bf16_v2<AK, BK, TC, true, 128, IMP>), grid, dim3(256), 0, st, g);
 }
