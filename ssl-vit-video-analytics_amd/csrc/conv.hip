@@ -168,6 +168,142 @@ __global__ __launch_bounds__(256, 4) void stem_conv1_kernel(ClipView v, int Ho, 
   }
 }
 
+// Band form (round 4): a block walks bands of SC1B_R output rows of one frame.  The band's
+// 2 R + 1 input rows of the three channels are first staged into LDS as bf16 with
+// coalesced loads (16-B loads of 4 consecutive pixels when the clip rows are contiguous and
+// aligned), each input element loaded once; the per-pixel 27-tap gathers then read LDS.
+// (The gathering kernel above loads every input ~2.25 times, half-coalesced at stride 2:
+// its waves waited on those loads 85 % of their cycles, profiles/r03q_stem_pmc.txt.)  The
+// A fragments, MFMA products and their order are the gathering kernel's, so a1 is
+// bit-identical; the BatchNorm-1 sums are taken in another order (fp32 rounding).
+constexpr int SC1B_R = 8, SC1B_NRI = 2 * SC1B_R + 1, SC1B_PADL = 4;
+
+__global__ __launch_bounds__(256, 2) void stem_conv1_band_kernel(ClipView v, int Ho, int Wo, const __bf16* w,
+                                                              __bf16* y, float* part, int vec4) {
+  extern __shared__ __attribute__((aligned(16))) char dyn[];
+  __shared__ __attribute__((aligned(16))) __bf16 img[4][32 * SC1_PITCH];
+  __shared__ float red[4][2][64];
+  const int WP = v.W + 2 * SC1B_PADL;                 // staged row pitch (bf16), zero pads both sides
+  __bf16* xs = (__bf16*)dyn;                          // [3][SC1B_NRI][WP]
+  const int l = threadIdx.x & 63, h = l >> 5, wv = threadIdx.x >> 6;
+  const int nbf = (Ho + SC1B_R - 1) / SC1B_R;
+  const int nbands = v.B * v.T * nbf;
+  bf16x8 wf[2][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int co = 32 * j + (l & 31);
+      if (co < SC1_COUT) wf[j][s] = *(const bf16x8*)(w + co * 32 + 16 * s + 8 * h);
+      else
+#pragma unroll
+        for (int e = 0; e < 8; ++e) wf[j][s][e] = (__bf16)0.f;
+    }
+  // zero pads (columns [0, PADL) and [PADL + W, WP) of every staged row): never overwritten
+  for (int i = threadIdx.x; i < 3 * SC1B_NRI * 2 * SC1B_PADL; i += 256) {
+    const int row = i / (2 * SC1B_PADL), c = i % (2 * SC1B_PADL);
+    xs[row * WP + (c < SC1B_PADL ? c : v.W + c)] = (__bf16)0.f;
+  }
+  // this lane's 16 taps (k = 16 s + 8 h + e): channel-row base and column offset, compile-time
+  // (k >= 27, the K padding: -1, read as zero)
+  int toff[2][8];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = 16 * s + e + 8 * h;
+      // staged row ci * NRI + ky (+ 2 ry), column kx - 1 + PADL (+ 2 xo)
+      toff[s][e] = k < 27 ? ((k / 9) * SC1B_NRI + (k % 9) / 3) * WP + k % 3 - 1 + SC1B_PADL : -1;
+    }
+  float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
+  __bf16* im = img[wv];
+  const int rowlen = SC1B_NRI * v.W;
+  for (int band = blockIdx.x; band < nbands; band += gridDim.x) {
+    const int f = band / nbf, yo0 = (band - f * nbf) * SC1B_R;
+    const int reff = min(SC1B_R, Ho - yo0);
+    const float* base = v.p + (int64_t)(f / v.T) * v.sB + (int64_t)(f % v.T) * v.sT;
+    const int yi0 = 2 * yo0 - 1;
+    __syncthreads();   // the previous band's gathers are done with xs
+    if (vec4) {        // sW == 1, W % 4 == 0, 16-B aligned rows
+      const int q = v.W >> 2;
+      for (int i = threadIdx.x; i < 3 * SC1B_NRI * q; i += 256) {
+        const int cr = i / q, x4 = (i - cr * q) * 4;
+        const int ci = cr / SC1B_NRI, r = cr - ci * SC1B_NRI, yi = yi0 + r;
+        float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
+        if ((unsigned)yi < (unsigned)v.H) val = *(const float4*)(base + ci * v.sC + (int64_t)yi * v.sH + x4);
+        bf16x4 b4 = {(__bf16)val.x, (__bf16)val.y, (__bf16)val.z, (__bf16)val.w};
+        *(bf16x4*)(xs + cr * WP + SC1B_PADL + x4) = b4;
+      }
+    } else {
+      for (int i = threadIdx.x; i < 3 * rowlen; i += 256) {
+        const int ci = i / rowlen, rem = i - ci * rowlen, r = rem / v.W, x = rem - r * v.W, yi = yi0 + r;
+        float val = 0.f;
+        if ((unsigned)yi < (unsigned)v.H) val = base[ci * v.sC + (int64_t)yi * v.sH + (int64_t)x * v.sW];
+        xs[(ci * SC1B_NRI + r) * WP + SC1B_PADL + x] = (__bf16)val;
+      }
+    }
+    __syncthreads();
+    const int npx = reff * Wo, nseg = (npx + 31) / 32;
+    const int64_t px0 = ((int64_t)f * Ho + yo0) * Wo;   // the band's first output pixel
+    for (int seg = wv; seg < nseg; seg += 4) {
+      const int p = min(seg * 32 + (l & 31), npx - 1);    // pixels past the band: recomputed, not stored
+      const int ry = p / Wo, xo = p - ry * Wo;
+      const int rb = 2 * ry * WP + 2 * xo;
+      bf16x8 af[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) af[s][e] = toff[s][e] >= 0 ? xs[toff[s][e] + rb] : (__bf16)0.f;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        f32x16 acc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], wf[j][s], acc, 0, 0, 0);
+        const int co = 32 * j + (l & 31);
+        if (co < SC1_COUT) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int pp = (r & 3) + 8 * (r >> 2) + 4 * h;
+            const __bf16 o = (__bf16)acc[r];
+            if (seg * 32 + pp < npx) {
+              const float of = (float)o;
+              s1[j] += of;
+              s2[j] = fmaf(of, of, s2[j]);
+            }
+            im[pp * SC1_PITCH + co] = o;
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int c = l + 64 * i, pp = c / 6, ch = c - pp * 6;
+        const uint4 val = *(const uint4*)(im + pp * SC1_PITCH + ch * 8);
+        if (seg * 32 + pp < npx) *(uint4*)(y + (px0 + seg * 32 + pp) * SC1_COUT + ch * 8) = val;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    s1[j] += __shfl_xor(s1[j], 32, 64);
+    s2[j] += __shfl_xor(s2[j], 32, 64);
+  }
+  if (h == 0) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      red[wv][0][32 * j + l] = s1[j];
+      red[wv][1][32 * j + l] = s2[j];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * SC1_COUT) {
+    const int which = threadIdx.x / SC1_COUT, co = threadIdx.x % SC1_COUT;
+    part[((int64_t)blockIdx.x * 2 + which) * SC1_COUT + co] =
+        ((red[0][which][co] + red[1][which][co]) + red[2][which][co]) + red[3][which][co];
+  }
+}
+
 // ------------------------------------------------------------------ stem conv2, direct
 // PatchEmbed conv2 (tiny_vit.py:69: 48 -> 96, 3x3, stride 1, pad 1) over h1 =
 // GELU(BN1(a1)) (tiny_vit.py:68) with BN2's statistics (tiny_vit.py:70): block = one
@@ -1687,11 +1823,23 @@ extern "C" int sm_stem_conv1_bn_stats(const float* clip, int B, int T, int H, in
   if (P >= (1LL << 31) - 64 || (int64_t)3 * sC >= (1LL << 31)) return -2;
   if (ws_bytes < sm_stem_conv1_workspace_bytes()) return -4;
   if ((((uintptr_t)wpack) | ((uintptr_t)y)) & 15) return -2;
-  const int64_t nseg = (P + 31) / 32;
-  const int nb = (int)std::min<int64_t>(SC1_BLOCKS, (nseg + 3) / 4);   // part rows
   float* part = (float*)ws;
   void* fin = (void*)(((uintptr_t)(part + (int64_t)SC1_BLOCKS * 2 * SC1_COUT) + 15) & ~(uintptr_t)15);
-  hipLaunchKernelGGL(stem_conv1_kernel, dim3(nb), dim3(256), 0, st, v, Ho, Wo, (const __bf16*)wpack, (__bf16*)y, part);
+  const size_t band_lds = (size_t)3 * SC1B_NRI * (W + 2 * SC1B_PADL) * 2;
+  int nb;
+  if (band_lds <= 48 * 1024) {   // band form: input rows staged through LDS
+    const int64_t nbands = (int64_t)B * T * ((Ho + SC1B_R - 1) / SC1B_R);
+    nb = (int)std::min<int64_t>(SC1_BLOCKS, nbands);
+    const int vec4 = sW == 1 && W % 4 == 0 && sH % 4 == 0 && sC % 4 == 0 && sT % 4 == 0 && sB % 4 == 0 &&
+                     (((uintptr_t)clip) & 15) == 0;
+    hipLaunchKernelGGL(stem_conv1_band_kernel, dim3(nb), dim3(256), band_lds, st, v, Ho, Wo, (const __bf16*)wpack,
+                       (__bf16*)y, part, vec4);
+  } else {
+    const int64_t nseg = (P + 31) / 32;
+    nb = (int)std::min<int64_t>(SC1_BLOCKS, (nseg + 3) / 4);   // part rows
+    hipLaunchKernelGGL(stem_conv1_kernel, dim3(nb), dim3(256), 0, st, v, Ho, Wo, (const __bf16*)wpack, (__bf16*)y,
+                       part);
+  }
   SM_CHECK_LAUNCH();
   return sm_bn_stats_from_partials(part, nb, SC1_COUT, P, mean, rstd, run_mean, run_var, num_batches_tracked,
                                    momentum, eps, updates, fin, 2 * SC1_COUT * 8, st);
