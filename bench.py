@@ -93,7 +93,7 @@ def cpu_baseline(T, S, ratio, B=4):
 
 
 PROBE_KERNELS = {"dec_attn_fwd": "attn_fwd_bf16<64, true>",
-                 "dec_attn_bwd": "attn_bwd_dq_bf16<64, true>+attn_bwd_dkdv_bf16<64, true>"}
+                 "dec_attn_bwd": "attn_bwd_dq_bf16<64, true, 4>+attn_bwd_dkdv_bf16<64, true, 4>"}
 def reference_cpu():
     """The reference's own train_one_epoch timed on the build container's CPU cores at
     BASELINE config 1 by scripts/ref_cpu_baseline.py (the reference cannot travel to
