@@ -1228,6 +1228,27 @@ __global__ __launch_bounds__(256, 2) void dwb2_kernel(const __bf16* dy, const __
   // frame-level views of x and dz (wave-uniform descriptors; see dwb_kernel)
   const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)(x + f * H * W * C), (short)0, H * W * C * 2, 0x00020000);
   const auto zr = __builtin_amdgcn_make_buffer_rsrc((void*)(dz + f * H * W * C), (short)0, H * W * C * 2, 0x00020000);
+  // item offsets; the thread's NEXT item's x is loaded while the current one computes
+  // (-2 % here, profiles/r04g_dwb_prefetch_ab.txt; the stride-1 kernel, already at 235
+  // VGPRs, spilled with it and lost 3 %)
+  auto item_offs = [&](int band_, int it_, uint32_t (&o)[PX]) {
+    const int ry = it_ / nstrip, strip = it_ - ry * nstrip;
+    const int xi_ = strip * PX;
+    const uint32_t b = (uint32_t)(((band_ * TYI + ry) * W + xi_) * C + c0) * 2u;
+#pragma unroll
+    for (int p = 0; p < PX; ++p) o[p] = (!RAG || xi_ + p < W) ? b + (uint32_t)(p * C * 2) : 0x80000000u;
+  };
+  auto xload = [&](const uint32_t (&o)[PX], bf16x4 (&xv)[PX]) {
+#pragma unroll
+    for (int p = 0; p < PX; ++p)
+      xv[p] = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(xr, o[p], 0, 0));
+  };
+  bf16x4 xn[PX];
+  {
+    uint32_t o[PX];
+    item_offs(0, t >> 3, o);
+    xload(o, xn);
+  }
   ring.stage_first<true>(lds, raw);
   for (int band = 0; band < nbands; ++band) {
     const int y0 = band * TYI, yo0 = band * DWB2_TYO;
@@ -1241,22 +1262,30 @@ __global__ __launch_bounds__(256, 2) void dwb2_kernel(const __bf16* dy, const __
     for (int it = t >> 3; it < items; it += 32) {
       const int ry = it / nstrip, strip = it - ry * nstrip;
       const int yi = y0 + ry;
-      if (yi >= H) continue;
       const int xi0 = strip * PX;
-      // pixels past W: out-of-range offset (loads read 0, stores are dropped)
-      const uint32_t off0 = (uint32_t)((yi * W + xi0) * C + c0) * 2u;
-      uint32_t offp[PX];
-#pragma unroll
-      for (int p = 0; p < PX; ++p) offp[p] = (!RAG || xi0 + p < W) ? off0 + (uint32_t)(p * C * 2) : 0x80000000u;
-      float h[PX][4], gg[PX][4], g[PX][4];
       bf16x4 xs[PX];
+#pragma unroll
+      for (int p = 0; p < PX; ++p) xs[p] = xn[p];
+      {
+        int nb = band, ni = it + 32;
+        if (ni >= items) {
+          nb = band + 1;
+          ni = t >> 3;
+        }
+        if (nb < nbands) {
+          uint32_t o[PX];
+          item_offs(nb, ni, o);
+          xload(o, xn);
+        }
+      }
+      if (yi >= H) continue;
+      uint32_t offp[PX];
+      item_offs(band, it, offp);
+      float h[PX][4], gg[PX][4], g[PX][4];
       {
         float sc[4], sh[4];
         load4(cl + c4 * 4, sc);
         load4(cl + DWF_CB + c4 * 4, sh);
-#pragma unroll
-        for (int p = 0; p < PX; ++p)
-          xs[p] = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(xr, offp[p], 0, 0));
 #pragma unroll
         for (int p = 0; p < PX; ++p) {
           const bool ok = !RAG || xi0 + p < W;

@@ -1125,7 +1125,12 @@ int choose_splits(int M, int N, int K, bool bf16) {
   const int64_t tiles = (int64_t)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   const int64_t slots = bf16 ? gemm_slots(v) : 512;
   if (tiles >= slots || K < 4096) return 1;
-  int64_t want = bf16 ? (2 * slots) / tiles : (1024 + tiles - 1) / tiles;
+  static const int rounds = [] {   // SM_GEMM_SPLIT_ROUNDS pins the round count (A/B runs)
+    const char* e = getenv("SM_GEMM_SPLIT_ROUNDS");
+    const int x = e ? atoi(e) : 0;
+    return (x >= 1 && x <= 64) ? x : 2;
+  }();
+  int64_t want = bf16 ? (rounds * slots) / tiles : (1024 + tiles - 1) / tiles;
   int64_t max_by_k = K / (4 * bk);
   int64_t s = want < max_by_k ? want : max_by_k;
   if (s > 2048) s = 2048;
