@@ -20,7 +20,7 @@ nsteps = len(ends) - a.skip
 
 
 def cat(n):
-    for key, c in (("gemm", "gemm"), ("splitk", "gemm"), ("attn_delta", "attn_delta"), ("dwf_", "dwconv"), ("dwb_", "dwconv"),
+    for key, c in (("gemm", "gemm"), ("splitk", "gemm"), ("attn_delta", "attn_delta"), ("dwf_", "dwconv"), ("dwb_", "dwconv"), ("dwb2_", "dwconv"),
                    ("dw_", "dwconv"), ("se_", "se"), ("bn_", "bn"), ("ln_", "ln"), ("gelu", "gelu"),
                    ("colsum", "colsum"), ("colred", "colsum"), ("im2col", "im2col"), ("col2im", "im2col"),
                    ("dropout", "dropout")):

@@ -157,12 +157,18 @@ SM_DEV bf16x8 lread_frag(const char* lds, int rb, int s) {
 // Row-staged stores (gemm_bf16_v2).  A row run is 8 consecutive columns of one output
 // row held by one lane; stored straight from the lanes, a store instruction covers 32
 // rows x 32 B (32 partial cache lines).  Staged, each wave writes its runs into a
-// 32-row x 128-B LDS image (chunk index XOR-swizzled with (row >> 1) & 7: conflict-free
-// both ways) and stores it back as 8 rows x 128 B per instruction (whole lines).
+// 32-row x 128-B LDS image and stores it back as 8 rows x 128 B per instruction (whole
+// lines).  Chunk index XOR-swizzled with rs_swz(row) = (row ^ row >> 3) & 7: the run
+// writes (8 consecutive rows per 8-lane ds_write_b128 group) hit 8 distinct chunk slots,
+// and the per-run reads (16 rows per ds_read_b128 group) and the 8 x 128-B flush reads
+// stay conflict-free.  (The earlier (row >> 1) & 7 put rows 2i and 2i + 1 on the same
+// banks: a 2-way conflict on every run write, 44 % extra LDS cycles in the stage-0
+// expand GEMM, profiles/r04g_gemm_sq_counters.txt.)
+SM_DEV int rs_swz(int row) { return (row ^ (row >> 3)) & 7; }
 struct RowStage {
   char* base;   // this wave's 2 x 4 KB: [0] C, [1] aux
   SM_DEV void put(int region, int row, int chunk, uint4 v) const {
-    *(uint4*)(base + region * 4096 + row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4)) = v;
+    *(uint4*)(base + region * 4096 + row * 128 + ((chunk ^ rs_swz(row)) << 4)) = v;
   }
   // rows: tile rows [row0, row0 + 32) of out (ld elements) at column col0; 16-B chunk
   // c holds `cpc` columns; rows >= M or chunk columns >= N are not stored
@@ -183,7 +189,7 @@ struct RowStage {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int r = (l >> 3) + 8 * q;
-      const uint4 v = *(const uint4*)(base + region * 4096 + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+      const uint4 v = *(const uint4*)(base + region * 4096 + r * 128 + ((c ^ rs_swz(r)) << 4));
       const int64_t row = row0 + r;
       const int col = col0 + c * cpc;
       if (row < M && col < N && c * cpc < wcols) {   // wcols: the wave's own columns of the image
@@ -335,7 +341,7 @@ SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int r = (l >> 3) + 8 * q;
-          *(uint4*)(stage + 4096 + r * 128 + ((c ^ ((r >> 1) & 7)) << 4)) = av[q];
+          *(uint4*)(stage + 4096 + r * 128 + ((c ^ rs_swz(r)) << 4)) = av[q];
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       }
@@ -382,7 +388,7 @@ SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x
           float pre[8];
           if (AUXS && sizeof(TC) == 2 && stage) {
             const int rr_ = l & 31, ch_ = 4 * j + 2 * p + h;
-            load8((const __bf16*)(stage + 4096 + rr_ * 128 + ((ch_ ^ ((rr_ >> 1) & 7)) << 4)), pre);
+            load8((const __bf16*)(stage + 4096 + rr_ * 128 + ((ch_ ^ rs_swz(rr_)) << 4)), pre);
           } else {
             load8((const TC*)g.aux + idx, pre);
           }
