@@ -1820,9 +1820,13 @@ __global__ __launch_bounds__(256) void se_bn_dx_kernel(const T* dy, const T* x, 
     else { typedef __bf16 T; __VA_ARGS__; }                    \
   } while (0)
 
+// every host-side Ho / Wo computation divides by the stride: only 1 and 2 exist
+static bool bad_stride(int s) { return s != 1 && s != 2; }
+
 extern "C" int sm_stem_im2col(int out_dtype, const float* clip, int B, int T, int H, int W, int64_t sB, int64_t sC,
                               int64_t sT, int64_t sH, int64_t sW, int stride, void* col, hipStream_t st) {
   ClipView v{clip, B, T, H, W, sB, sC, sT, sH, sW};
+  if (bad_stride(stride)) return -2;
   const int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
   const int64_t P = (int64_t)B * T * Ho * Wo;
   if (P <= 0) return 0;
@@ -1898,6 +1902,7 @@ extern "C" int sm_stem_conv2_bn_stats(const void* a1, int F, int H, int W, const
 extern "C" int sm_im2col3(int dtype, const void* x, int F, int H, int W, int C, int stride, void* col,
                           hipStream_t st) {
   if (C % 8) return -2;
+  if (bad_stride(stride)) return -2;
   const int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
   const int64_t total = (int64_t)F * Ho * Wo * 9 * (C / 8);
   if (total <= 0) return 0;
@@ -1910,6 +1915,7 @@ extern "C" int sm_im2col3(int dtype, const void* x, int F, int H, int W, int C, 
 extern "C" int sm_col2im3(int dtype, const void* dcol, int F, int H, int W, int C, int stride, void* dx,
                           hipStream_t st) {
   if (C % 8) return -2;
+  if (bad_stride(stride)) return -2;
   const int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
   const int64_t total = (int64_t)F * H * W * (C / 8);
   if (total <= 0) return 0;
@@ -1941,6 +1947,7 @@ extern "C" int sm_conv_wunpack_add(const float* packed, float* grad, int Cout, i
 extern "C" int sm_dwconv_fwd(int dtype, const void* x, const float* w, void* y, int F, int H, int W, int C,
                              int stride, hipStream_t st) {
   if (C % 8) return -2;
+  if (bad_stride(stride)) return -2;
   const int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
   const int64_t total = (int64_t)F * Ho * ((Wo + DW_PX - 1) / DW_PX) * (C / 8);
   if (total <= 0) return 0;
@@ -1978,6 +1985,7 @@ extern "C" int sm_dwconv_fused_fwd(int F, int H, int W, int C, int stride, const
                                    const float* w, void* y, float* part, hipStream_t st) {
   if (!dwf_shape_ok(F, W, C, stride)) return -2;
   if (((uintptr_t)w & 15) || ((uintptr_t)x & 15) || ((uintptr_t)y & 15)) return -2;
+  if (bad_stride(stride)) return -2;
   const int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
   ChanAffine act{in_mean, in_rstd, in_w, in_b, in_gelu};
   const dim3 grid((C / DWF_CB) * F);
@@ -2017,6 +2025,7 @@ extern "C" int sm_dwconv_fused_bwd(int F, int H, int W, int C, int stride, const
                                    hipStream_t st) {
   if (!dwf_shape_ok(F, W, C, stride)) return -2;
   if (ws_bytes < sm_dwconv_fused_bwd_workspace_bytes(F, H, W, C, stride)) return -4;
+  if (bad_stride(stride)) return -2;
   const int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
   const size_t lds = dwf_lds_bytes(W, stride);
   float* part = (float*)ws;
@@ -2056,6 +2065,7 @@ static int dwconv_bn_bwd(int stride, int F, int H, int W, int C, const void* dy,
                          const float* bn_rstd, const float* bn_w, const float* bn_b, int bn_gelu, const float* w,
                          void* dx, float* dw, float* dgamma, float* dbeta, void* ws, int64_t ws_bytes,
                          hipStream_t st) {
+  if (bad_stride(stride)) return -2;
   const int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
   size_t lds = stride == 1 ? dwf_lds_bytes(W, 1) + DWB_PAD + 4 * DWF_CB * 4
                            : (size_t)DwRing<1, DWB2_TYO>::NR * (Wo + 2) * 64 + DWB2_PAD + 13 * DWF_CB * 4;
@@ -2122,6 +2132,7 @@ extern "C" int sm_dwconv_s2_bn_bwd(int F, int H, int W, int C, const void* dy, c
 }
 
 extern "C" int64_t sm_dwconv_wgrad_workspace_bytes(int F, int H, int W, int C, int stride) {
+  if (bad_stride(stride)) return 0;
   const int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
   const int64_t P = (int64_t)F * Ho * Wo;
   int64_t ppb = (P + 1023) / 1024;
@@ -2133,6 +2144,7 @@ extern "C" int64_t sm_dwconv_wgrad_workspace_bytes(int F, int H, int W, int C, i
 extern "C" int sm_dwconv_bwd(int dtype, const void* dy, const void* x, const float* w, void* dx, float* dw, int F,
                              int H, int W, int C, int stride, void* ws, int64_t ws_bytes, hipStream_t st) {
   if (C % 8 || C / 8 > 256) return -2;
+  if (bad_stride(stride)) return -2;
   const int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
   const int64_t P = (int64_t)F * Ho * Wo;
   if (P <= 0) return 0;

@@ -81,6 +81,7 @@ extern "C" int sm_fedavg_weighted_sum(int num_clients, const float* const* clien
                                       int64_t n, float* out, hipStream_t st) {
   if (num_clients < 1 || num_clients > kMaxClients || n < 0) return -2;
   if (n == 0) return 0;
+  if (!client_bufs || !weights || !out) return -2;
   ClientPtrs c{};
   bool vec = aligned16(out);
   for (int j = 0; j < num_clients; ++j) {
@@ -120,6 +121,7 @@ extern "C" int sm_fedavg_counters_max(int num_clients, const int64_t* const* cli
                                       int64_t* out, hipStream_t st) {
   if (num_clients < 1 || num_clients > kMaxClients || n < 0) return -2;
   if (n == 0) return 0;
+  if (!client_counters || !out) return -2;
   ClientCounters c{};
   for (int j = 0; j < num_clients; ++j) {
     if (!client_counters[j]) return -2;

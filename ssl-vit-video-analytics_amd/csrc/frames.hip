@@ -87,6 +87,7 @@ extern "C" int sm_frames_normalize(const uint8_t* frames, const uint8_t* valid, 
   if (B < 0 || T < 0 || H < 0 || W < 0) return -2;
   const int64_t hw = (int64_t)H * W, total = (int64_t)B * T * hw;
   if (total == 0) return 0;
+  if (!frames || !mean3 || !std3 || !out) return -2;   // (mean3 / std3 are host arrays)
   Norm nm;
   for (int c = 0; c < 3; ++c) {
     nm.mean[c] = mean3[c];
