@@ -152,6 +152,22 @@ SM_DEV uint32_t pack_bf16x2(float lo, float hi) {
   return __builtin_bit_cast(uint32_t, v);
 }
 
+// Row-per-lane epilogue of a 32x32 accumulator tile (lane l: row l & 31; half-wave h = l >> 5
+// holds columns 8g + 4h .. + 3 of 8-column group g): each pair of groups (g, g + 1) leaves as
+// ONE 16-B store per lane instead of two 8-B stores (MI355X guide T21: the tail is bound by
+// store issue, not bytes).  Two v_permlane32_swap per pair hand the lower half-wave the upper
+// half's columns of group g and the upper half the lower half's of group g + 1: the lower
+// lanes then hold columns 8g .. 8g + 7, the upper lanes 8g + 8 .. 8g + 15.  Every lane must
+// execute it (EXEC full: the swap reads the partner lane); the caller predicates the store.
+// va / vb: this lane's 4 values of groups g / g + 1; returns the 16 B for column 8 (g + h).
+SM_DEV uint4 wide_pair(const float (&va)[4], const float (&vb)[4]) {
+  const uint32_t a0 = pack_bf16x2(va[0], va[1]), a1 = pack_bf16x2(va[2], va[3]);
+  const uint32_t b0 = pack_bf16x2(vb[0], vb[1]), b1 = pack_bf16x2(vb[2], vb[3]);
+  const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+  const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+  return make_uint4(r0[0], r1[0], r0[1], r1[1]);
+}
+
 // dropout keep multiplier for P[n,hd,q,k] (f32 kernels)
 SM_DEV float drop_keep_scale(const AttnArgs& a, int n, int hd, int q, int k) {
   const uint64_t row = (uint64_t)(n * a.H + hd) * a.L + q;
@@ -406,19 +422,23 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(AttnArgs a) {
   if (wact && __any(bad && q < a.L) && l == 0) lbad = 1;
   __syncthreads();
   if (lbad) pass(std::true_type{});   // block-uniform: the rerun's barriers are safe
-  if (q < a.L) {
+  {
     const float inv = (DROP ? 1.f / (1.f - a.drop_p) : 1.f) / lsum;
     __bf16* ob = (__bf16*)a.out + ((int64_t)n * a.L + q) * C + hd * D;
 #pragma unroll
     for (int t = 0; t < D / 32; ++t)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        float v[4];
+      for (int g = 0; g < 4; g += 2) {
+        float va[4], vb[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = o[t][4 * g + i] * inv;
-        store4(ob + 32 * t + 8 * g + 4 * h, v);
+        for (int i = 0; i < 4; ++i) {
+          va[i] = o[t][4 * g + i] * inv;
+          vb[i] = o[t][4 * g + 4 + i] * inv;
+        }
+        const uint4 w16 = wide_pair(va, vb);
+        if (q < a.L) *(uint4*)(ob + 32 * t + 8 * g + 8 * h) = w16;
       }
-    if (h == 0) a.lse[((int64_t)n * a.H + hd) * a.L + q] = (m + log2f(lsum)) * LN2;
+    if (q < a.L && h == 0) a.lse[((int64_t)n * a.H + hd) * a.L + q] = (m + log2f(lsum)) * LN2;
   }
 }
 
@@ -616,17 +636,25 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_bf16(AttnArgs a
     softmax(q0, 1, s1, p1, pf1, sf1);
     dvdk(1, pf1, sf1);
   }
-  if (key < a.L) {
+  {
     __bf16* out = (__bf16*)a.out + ((int64_t)n * a.L + key) * ldq + hd * D;
 #pragma unroll
     for (int t = 0; t < D / 32; ++t)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        float vk[4], vv[4];
+      for (int g = 0; g < 4; g += 2) {
+        float ka[4], kb2[4], va[4], vb[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) { vk[i] = dk[t][4 * g + i] * LN2; vv[i] = dv[t][4 * g + i]; }
-        store4(out + C + 32 * t + 8 * g + 4 * h, vk);
-        store4(out + 2 * C + 32 * t + 8 * g + 4 * h, vv);
+        for (int i = 0; i < 4; ++i) {
+          ka[i] = dk[t][4 * g + i] * LN2;
+          kb2[i] = dk[t][4 * g + 4 + i] * LN2;
+          va[i] = dv[t][4 * g + i];
+          vb[i] = dv[t][4 * g + 4 + i];
+        }
+        const uint4 wk = wide_pair(ka, kb2), wv = wide_pair(va, vb);
+        if (key < a.L) {
+          *(uint4*)(out + C + 32 * t + 8 * g + 8 * h) = wk;
+          *(uint4*)(out + 2 * C + 32 * t + 8 * g + 8 * h) = wv;
+        }
       }
   }
 }
@@ -758,16 +786,20 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_bf16(AttnArgs a) 
   int k0 = 0;
   for (; k0 + KT <= a.L; k0 += KT) tile(k0, std::false_type{});
   if (k0 < a.L) tile(k0, std::true_type{});
-  if (qok) {
+  {
     __bf16* out = (__bf16*)a.out + ((int64_t)n * a.L + q) * ldq + hd * D;
 #pragma unroll
     for (int t = 0; t < D / 32; ++t)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        float v[4];
+      for (int g = 0; g < 4; g += 2) {
+        float va[4], vb[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = dq[t][4 * g + i] * a.scale;
-        store4(out + 32 * t + 8 * g + 4 * h, v);
+        for (int i = 0; i < 4; ++i) {
+          va[i] = dq[t][4 * g + i] * a.scale;
+          vb[i] = dq[t][4 * g + 4 + i] * a.scale;
+        }
+        const uint4 w16 = wide_pair(va, vb);
+        if (qok) *(uint4*)(out + 32 * t + 8 * g + 8 * h) = w16;
       }
   }
 }
