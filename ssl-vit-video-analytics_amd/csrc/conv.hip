@@ -322,7 +322,7 @@ constexpr int SC2_PXS = 130, SC2_PITCH = 56, SC2_WPITCH = 440;   // bf16 units
 constexpr int SC2_NW = 12, SC2_NT = SC2_NW * 64, SC2_CHUNKS = 2;  // staged 16-B chunks per thread per band
 constexpr int SC2_RING = SC2_NR * SC2_PXS * SC2_PITCH * 2, SC2_LDS = SC2_RING + SC2_COUT * SC2_WPITCH * 2;
 
-template <bool GELU>
+template <bool GELU, bool STAGED>
 __global__ __launch_bounds__(SC2_NT, 1) void stem_conv2_kernel(const __bf16* a1, ChanAffine act,
                                                                const __bf16* wpack /*[96][432]*/, __bf16* y,
                                                                float* part /*[F][2][96]*/, int H, int W) {
@@ -397,6 +397,7 @@ __global__ __launch_bounds__(SC2_NT, 1) void stem_conv2_kernel(const __bf16* a1,
     if (cpos[i] >= 0 && (cpos[i] >> 16) == 0) commit_chunk(i, SC2_R);
   float s1 = 0.f, s2 = 0.f;   // BN2 sums of channel 32 nb + (l & 31) over this lane's pixels
   const int nbands = (H + SC2_R - 1) / SC2_R;
+  constexpr bool staged = STAGED;   // host: W >= 110 (stem_conv2_staged)
   const int co = 32 * nb + (l & 31);
   const __bf16* wrow = wl + co * SC2_WPITCH + 8 * h;
   for (int band = 0; band < nbands; ++band) {
@@ -432,22 +433,42 @@ __global__ __launch_bounds__(SC2_NT, 1) void stem_conv2_kernel(const __bf16* a1,
       }
       __builtin_amdgcn_sched_barrier(0);   // one tap row's fragments in flight (registers)
     }
+    // Output tile: lane = channel co, registers = pixels (r & 3) + 8 (r >> 2) + 4 h of the
+    // segment.  Staged (W >= 110, the 112-pixel stem): the tile goes through LDS -- the ring
+    // slots of rows y0 - 1 and y0 are dead once every wave has finished this band's MFMAs
+    // (one barrier), and the next band's commit rewrites every byte used here (pixel columns
+    // 1 .. W; halo columns and the 16-B pad reads never touched) -- and leaves as 16-B stores of
+    // 8 channels of one pixel: 2 store instructions per row and wave where the direct form
+    // issued 16 2-byte stores (each two 64-B runs).  Direct form: narrow frames.
+    char* stg = nullptr;
+    if (staged) {
+      __syncthreads();
+      stg = (char*)(ring + (slot(wv < SC2_NW / 2 ? y0 - 1 : y0) * SC2_PXS + 1) * SC2_PITCH) + (wv % (SC2_NW / 2)) * 2048;
+    }
 #pragma unroll
     for (int yy = 0; yy < SC2_R; ++yy) {
       const int yo = y0 + yy;
       if (yo >= H) break;
-      // lane = channel co, registers = pixels (r & 3) + 8 (r >> 2) + 4 h of the segment:
-      // each store instruction writes two 64-B runs (channels 32 nb .. + 31 of two pixels)
       __bf16* yr = y + ((f * H + yo) * W + sg * 32) * SC2_COUT + co;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int pp = (r & 3) + 8 * (r >> 2) + 4 * h;
         const __bf16 o = (__bf16)acc[yy][r];
+        if (staged) *(__bf16*)(stg + pp * 64 + (l & 31) * 2) = o;   // [pixel][32 channels]
         if (sg * 32 + pp < W) {
           const float of = (float)o;
           s1 += of;
           s2 = fmaf(of, of, s2);
-          yr[pp * SC2_COUT] = o;
+          if (!staged) yr[pp * SC2_COUT] = o;
+        }
+      }
+      if (staged) {   // lane l: pixels (l >> 2) + 16 k, channels 32 nb + 8 (l & 3) .. + 7
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int px = (l >> 2) + 16 * k;
+          const uint4 v = *(const uint4*)(stg + px * 64 + (l & 3) * 16);
+          if (sg * 32 + px < W)
+            *(uint4*)(y + ((f * H + yo) * W + sg * 32 + px) * SC2_COUT + 32 * nb + 8 * (l & 3)) = v;
         }
       }
     }
@@ -1891,7 +1912,10 @@ extern "C" int sm_stem_conv2_bn_stats(const void* a1, int F, int H, int W, const
   if (ws_bytes < sm_stem_conv2_workspace_bytes(F)) return -4;
   float* part = (float*)ws;
   void* fin = (void*)(((uintptr_t)(part + (int64_t)F * 2 * SC2_COUT) + 15) & ~(uintptr_t)15);
-  auto kern = gelu ? stem_conv2_kernel<true> : stem_conv2_kernel<false>;
+  // staged epilogue: its LDS image must fit in pixel columns 1 .. W of a ring slot
+  const bool staged = (int64_t)(W + 1) * SC2_PITCH * 2 >= SC2_PITCH * 2 + (SC2_NW / 2) * 2048;
+  auto kern = gelu ? (staged ? stem_conv2_kernel<true, true> : stem_conv2_kernel<true, false>)
+                   : (staged ? stem_conv2_kernel<false, true> : stem_conv2_kernel<false, false>);
   hipLaunchKernelGGL(kern, dim3(F), dim3(SC2_NT), 0, st, (const __bf16*)a1,
                      ChanAffine{bn1_mean, bn1_rstd, bn1_w, bn1_b, gelu}, (const __bf16*)wpack, (__bf16*)y, part, H, W);
   SM_CHECK_LAUNCH();

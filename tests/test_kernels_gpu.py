@@ -902,13 +902,15 @@ def test_stem_conv1_direct(shape, frames):
 
 
 @pytest.mark.parametrize("Fn,H,W,gelu", [(3, 14, 12, True), (2, 9, 23, True), (32, 112, 112, True),
-                                         (1, 5, 128, True), (2, 1, 7, False), (3, 3, 33, False)])
+                                         (1, 5, 128, True), (2, 1, 7, False), (3, 3, 33, False),
+                                         (2, 7, 110, True), (1, 4, 109, False)])
 def test_stem_conv2_direct(Fn, H, W, gelu):
     """Stem conv2 over act(a1) with BN1 (+GELU) applied in the kernel's LDS ring
     (sm_stem_conv2_bn_stats): y bit-identical to conv3x3_fwd(bn_apply(a1)) (same k order
     and MFMA chain), BN2 statistics / running statistics within fp32 rounding.  Shapes:
     ragged pixel segments (W = 12, 23, 33), the bench frame (112^2, 32 frames), the widest
-    frame (W = 128), a single row (H = 1), odd band counts; identity activation."""
+    frame (W = 128), a single row (H = 1), odd band counts; identity activation.  W >= 110
+    takes the LDS-staged 16-B-store epilogue (W = 110 its smallest frame, 109 the direct form)."""
     kk = KK()
     g = torch.Generator().manual_seed(230)
     a1 = (torch.randn(Fn * H * W, 48, generator=g) * 2).to(torch.bfloat16).to(DEV)
