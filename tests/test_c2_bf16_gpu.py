@@ -113,10 +113,10 @@ def test_decoder_attention_d64_full_L(p):
     _check_heads(qkv, dO, o, dqkv, N, L, H, D, p, seed, [(0, 0), (1, 5), (1, 2)])
 
 
-@pytest.mark.parametrize("N,L,H", [(4, 3136, 6), (8, 784, 12)])
+@pytest.mark.parametrize("N,L,H", [(4, 3136, 6), (8, 784, 12), (2, 2100, 3)])
 def test_encoder_attention_d32_full_L(N, L, H):
     """Encoder global attention of stage 1 (56^2 = 3136 tokens, 6 heads) and stage 2
-    (28^2 = 784 tokens, 12 heads), d = 32, no dropout."""
+    (28^2 = 784 tokens, 12 heads), d = 32, no dropout; L = 2100 is a ragged long sequence (partial last 128-row block)."""
     D = 32
     qkv = _randn((N * L, 3 * H * D), 3 + L)
     dO = _randn((N * L, H * D), 4 + L)
