@@ -213,24 +213,39 @@ struct LnBranch {
   int64_t rpg;
 };
 
+// C = 384 runs 32 lanes per row (2 rows per wave, 8 per block in flight): 3 chunks of 4
+// columns per lane, as at C = 192, instead of 6 -- the 16-lane form held xhat, gamma dy and
+// the dgamma / dbeta partials of 24 columns per lane (188 VGPRs, 2 waves per SIMD; 3.9-4.1
+// TB/s where the C = 192 form, 116 VGPRs and 4 waves, streams at 5.2).
+template <int C>
+constexpr int ln_bwd_lanes() { return C >= 384 ? 32 : 16; }
+
 template <typename TI, typename TD, int C>
 __global__ __launch_bounds__(256) void ln_bwd16_kernel(const TD* dy, const TI* x, const float* mean,
                                                        const float* rstd, const float* g, TI* dx, float* part_g,
                                                        float* part_b, int64_t M, int64_t rows_per_block,
                                                        const TI* dres, LnBranch br) {
-  constexpr int U = C / 64;
+  constexpr int G = ln_bwd_lanes<C>();   // lanes per row
+  constexpr int U = C / (4 * G);         // 4-column chunks per lane, columns 4G u + 4 gl + j
+  constexpr int RG = 256 / G;            // rows of a block in flight
+  static_assert(U * 4 * G == C, "C must split over the row's lanes");
   __shared__ float red[2][4][C];
-  const int gl = threadIdx.x & 15, grp = threadIdx.x >> 4, w = threadIdx.x >> 6;
+  const int gl = threadIdx.x & (G - 1), grp = threadIdx.x / G, w = threadIdx.x >> 6;
   float gw[U][4], ag[U][4], ab[U][4];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    load4(g + 64 * u + 4 * gl, gw[u]);
+    load4(g + 4 * G * u + 4 * gl, gw[u]);
 #pragma unroll
     for (int j = 0; j < 4; ++j) { ag[u][j] = 0.f; ab[u][j] = 0.f; }
   }
+  auto row_sum = [](float v) {
+    v = sum16(v);
+    if constexpr (G == 32) v += __shfl_xor(v, 16, 64);
+    return v;
+  };
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = min(M, r0 + rows_per_block);
-  for (int64_t row = r0 + grp; row < r1; row += 16) {
+  for (int64_t row = r0 + grp; row < r1; row += RG) {
     const float mu = mean[row], rs = rstd[row];
     const int64_t e0 = row * C + 4 * gl;
     float xh[U][4], gy[U][4];
@@ -238,8 +253,8 @@ __global__ __launch_bounds__(256) void ln_bwd16_kernel(const TD* dy, const TI* x
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       float xv[4], dv[4];
-      load4(x + e0 + 64 * u, xv);
-      load4(dy + e0 + 64 * u, dv);
+      load4(x + e0 + 4 * G * u, xv);
+      load4(dy + e0 + 4 * G * u, dv);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         xh[u][j] = (xv[j] - mu) * rs;
@@ -250,8 +265,8 @@ __global__ __launch_bounds__(256) void ln_bwd16_kernel(const TD* dy, const TI* x
         ab[u][j] += dv[j];
       }
     }
-    s1 = sum16(s1) * (1.f / C);
-    s2 = sum16(s2) * (1.f / C);
+    s1 = row_sum(s1) * (1.f / C);
+    s2 = row_sum(s2) * (1.f / C);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       float o[4];
@@ -259,16 +274,16 @@ __global__ __launch_bounds__(256) void ln_bwd16_kernel(const TD* dy, const TI* x
       for (int j = 0; j < 4; ++j) o[j] = rs * (gy[u][j] - s1 - xh[u][j] * s2);
       if (dres) {
         float pr[4];
-        load4(dres + e0 + 64 * u, pr);
+        load4(dres + e0 + 4 * G * u, pr);
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[j] += pr[j];
       }
-      store4(dx + e0 + 64 * u, o);
+      store4(dx + e0 + 4 * G * u, o);
       if (br.bo) {
         const float rsv = br.rs ? br.rs[row / br.rpg] : 1.f;
         const float ks = br.p > 0.f ? 1.f / (1.f - br.p) : 1.f;
         const uint32_t hsh = br.p > 0.f ? drop_hash(drop_rowbase(seed32(br.seed), (uint64_t)row),
-                                                     (uint32_t)(64 * u + 4 * gl)) : 0u;
+                                                     (uint32_t)(4 * G * u + 4 * gl)) : 0u;
         const uint32_t thr = drop_thr(br.p);
         float b4[4];
 #pragma unroll
@@ -277,30 +292,32 @@ __global__ __launch_bounds__(256) void ln_bwd16_kernel(const TD* dy, const TI* x
           const float mj = br.p > 0.f ? (((hsh >> (8 * j)) & 0xFFu) >= thr ? ks : 0.f) : 1.f;
           b4[j] = d * (rsv * mj);
         }
-        store4(br.bo + e0 + 64 * u, b4);
+        store4(br.bo + e0 + 4 * G * u, b4);
       }
     }
   }
-  // column partials: the 4 row groups of a wave, then the 4 waves (fixed order)
+  // column partials: the row groups of a wave, then the 4 waves (fixed order)
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float a = ag[u][j], c = ab[u][j];
-      a += __shfl_xor(a, 16, 64);
-      c += __shfl_xor(c, 16, 64);
+      if constexpr (G == 16) {
+        a += __shfl_xor(a, 16, 64);
+        c += __shfl_xor(c, 16, 64);
+      }
       a += __shfl_xor(a, 32, 64);
       c += __shfl_xor(c, 32, 64);
       ag[u][j] = a;
       ab[u][j] = c;
     }
-  if ((threadIdx.x & 63) < 16) {
+  if ((threadIdx.x & 63) < G) {
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        red[0][w][64 * u + 4 * gl + j] = ag[u][j];
-        red[1][w][64 * u + 4 * gl + j] = ab[u][j];
+        red[0][w][4 * G * u + 4 * gl + j] = ag[u][j];
+        red[1][w][4 * G * u + 4 * gl + j] = ab[u][j];
       }
   }
   __syncthreads();
