@@ -1789,7 +1789,11 @@ __global__ void se_bn_finalize_kernel(const double* sums, int64_t M, int C, floa
   coef[C + c] = (float)(b / (double)M);
 }
 
-// da2 = w rstd (du - mean(du) - xhat mean(du xhat)),  du = (dh3 s + dpool/HW) GELU'(u)
+// da2 = w rstd (du - mean(du) - xhat mean(du xhat)),  du = (dh3 s + dpool/HW) GELU'(u),
+// expanded per (frame, channel) into da2 = GELU'(u) (dh3 A + B) + c0 - c1 x with
+// A = w rstd s, B = w rstd dpool/HW, c1 = w rstd^2 mean(du xhat), c0 = w rstd (mean rstd
+// mean(du xhat) - mean(du)): 6 constants per channel instead of 9 (the 9 held 72 VGPRs
+// and the kernel at 4 waves per SIMD)
 template <typename T>
 __global__ __launch_bounds__(256) void se_bn_dx_kernel(const T* dy, const T* x, ChanAffine act, const float* s,
                                                        const float* dpool, const float* coef, T* dx, int HW,
@@ -1799,17 +1803,19 @@ __global__ __launch_bounds__(256) void se_bn_dx_kernel(const T* dy, const T* x, 
   const int k = blockIdx.x;
   const int64_t f = blockIdx.y;
   const int p0 = k * SE_PX_PER_SPLIT, p1 = min(HW, p0 + SE_PX_PER_SPLIT);
-  BnCh8 bc;
-  bc.init(act, cm.c0);
-  float ss[8], ad[8], k0[8], k1[8];
+  float sc[8], sh[8], ka[8], kb[8], c0[8], c1[8];
   const float inv = 1.f / (float)HW;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int c = cm.c0 + j;
-    ss[j] = s[f * C + c];
-    ad[j] = dpool[f * C + c] * inv;
-    k0[j] = coef[c];
-    k1[j] = coef[C + c];
+    const float rs = act.rstd[c], mu = act.mean[c];
+    sc[j] = rs * act.w[c];
+    sh[j] = bn_shift(act.b[c], mu, sc[j]);
+    const float wr = act.w[c] * rs, k1 = coef[C + c];
+    ka[j] = wr * s[f * C + c];
+    kb[j] = wr * (dpool[f * C + c] * inv);
+    c1[j] = wr * k1 * rs;
+    c0[j] = wr * (k1 * (mu * rs) - coef[c]);
   }
   for (int p = p0 + cm.r; p < p1; p += cm.rpp) {
     const int64_t e = (f * HW + p) * C + cm.c0;
@@ -1820,14 +1826,10 @@ __global__ __launch_bounds__(256) void se_bn_dx_kernel(const T* dy, const T* x, 
     for (int j = 0; j < 8; j += 2) {   // packed pairs (gelu_phi_pair_t)
       f32x2 gd = f32x2{1.f, 1.f};
       if (act.gelu)
-        gd = gelu_grad2(vfma(f32x2{v[j], v[j + 1]}, f32x2{bc.sc[j], bc.sc[j + 1]}, f32x2{bc.sh[j], bc.sh[j + 1]}));
+        gd = gelu_grad2(vfma(f32x2{v[j], v[j + 1]}, f32x2{sc[j], sc[j + 1]}, f32x2{sh[j], sh[j + 1]}));
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const float xh = fmaf(v[j + i], bc.rs[j + i], -bc.mr[j + i]);
-        float du = fmaf(g[j + i], ss[j + i], ad[j + i]);
-        if (act.gelu) du *= gd[i];
-        o[j + i] = bc.wr[j + i] * (du - k0[j + i] - xh * k1[j + i]);
-      }
+      for (int i = 0; i < 2; ++i)
+        o[j + i] = fmaf(gd[i], fmaf(g[j + i], ka[j + i], kb[j + i]), fmaf(-c1[j + i], v[j + i], c0[j + i]));
     }
     store8(dx + e, o);
   }
