@@ -40,6 +40,12 @@ int sm_gemm(int ab_dtype, int c_dtype, int a_layout, int b_layout, int M, int N,
             const float* bias, float alpha, float beta, int epi, void* aux, const void* R,
             float drop_p, uint64_t seed, const float* row_scale, int64_t rows_per_group,
             void* workspace, int64_t ws_bytes, hipStream_t stream);
+/* Form of the non-split bf16 GEMMs with a K-major A and a plain bf16 epilogue (every
+ * forward / data-gradient Linear of the step): 1 = persistent blocks with each tile's
+ * output stores drained under the next tile's K loop (default; SM_GEMM_PP=0 in the
+ * environment starts the process with 0), 0 = one tile per block.  Outputs are
+ * bit-identical either way.  mode < 0 only queries.  Returns the previous mode. */
+int sm_gemm_persistent(int mode);
 /* Weight + bias gradient of y = x W^T + b (Linear / 1x1 conv backward, e.g.
  * tiny_vit.py:74-84 Mlp, mae_vit_adapter.py:40-48 decoder layers): dW[nout][nin]
  * (+)= dy^T x and db[nout] += sum_rows dy in one GEMM pass over dy (bf16 dy, x;
@@ -47,18 +53,18 @@ int sm_gemm(int ab_dtype, int c_dtype, int a_layout, int b_layout, int M, int N,
 int64_t sm_linear_dw_bias_workspace_bytes(int rows, int nout, int nin);
 int sm_linear_dw_bias(int rows, int nout, int nin, const void* dy, const void* x, float* dW, float* db,
                       int accumulate, void* ws, int64_t ws_bytes, hipStream_t stream);
-/* fc2's weight gradient with the activation formed in the GEMM's operand loads:
- * dW[nout][nin] (+)= dy^T dropout(GELU(pre)), db += colsum(dy); pre = the fc1
- * pre-activation [rows][nin] bf16, (drop_p, seed) the fc1 output's dropout (the Mlp of
- * tiny_vit.py:74-84, the decoder feed-forward).  Bit-identical to sm_gelu_fwd followed by
- * sm_linear_dw_bias without the recompute pass; workspace as
- * sm_linear_dw_bias_workspace_bytes. */
 /* The fc2 data gradient through dropout(GELU(pre)) with the fc2 weight gradient's operand
  * as a side output (Mlp tiny_vit.py:74-84, decoder FF mae_vit_adapter.py:40-48): dx = (dy w)
  * * keep / (1 - p) * GELU'(pre) and h = bf16(GELU(pre) * keep / (1 - p)) (= sm_gelu_fwd(pre))
  * from one epilogue.  dy [M][N], w [N][K], pre / dx / h [M][K] bf16; N, K % 8 == 0. */
 int sm_linear_dx_gelu(int M, int N, int K, const void* dy, const void* w, const void* pre, void* dx, void* h,
                       float drop_p, uint64_t seed, hipStream_t stream);
+/* fc2's weight gradient with the activation formed in the GEMM's operand loads:
+ * dW[nout][nin] (+)= dy^T dropout(GELU(pre)), db += colsum(dy); pre = the fc1
+ * pre-activation [rows][nin] bf16, (drop_p, seed) the fc1 output's dropout (the Mlp of
+ * tiny_vit.py:74-84, the decoder feed-forward).  Bit-identical to sm_gelu_fwd followed by
+ * sm_linear_dw_bias without the recompute pass; workspace as
+ * sm_linear_dw_bias_workspace_bytes. */
 int sm_linear_dw_bias_gelu(int rows, int nout, int nin, const void* dy, const void* pre, float drop_p,
                            uint64_t seed, float* dW, float* db, int accumulate, void* ws, int64_t ws_bytes,
                            hipStream_t stream);

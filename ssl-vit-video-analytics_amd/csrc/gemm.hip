@@ -600,8 +600,7 @@ SM_DEV __amdgpu_buffer_rsrc_t panel_rsrc(const __bf16* P, int64_t off) {
 }
 
 template <bool KMAJ, int ROWS>
-SM_DEV bf16x8 lread_frag_r(const char* lds, int rb, int s) {
-  const int l = threadIdx.x & 63;
+SM_DEV bf16x8 lread_frag_r(const char* lds, int rb, int s, int l = threadIdx.x & 63) {
   if (KMAJ) {
     return *(const bf16x8*)(lds + kmaj_off(rb + (l & 31), 2 * s + (l >> 5)));
   } else {
@@ -1012,6 +1011,336 @@ __global__ __launch_bounds__(BMV * 2, (BMV == 256 && IMP != 5 && IMP != 6 && IMP
                                                                            lds + w * 8192);
 }
 
+// ============================================================ bf16 GEMM, persistent + pipelined
+// gemm_bf16_pp: v2's tile (256 x 128 x 64 on 8 waves of 64 x 64, the same operand images,
+// fragment reads, MFMA order and elementwise epilogue: outputs bit-identical to v2) in
+// persistent blocks that walk their XCD group's tiles.  Between two tiles:
+//   1. the epilogue math writes the finished tile into LDS (the dead operand area: each wave
+//      its own 2 x 4 KB row images) -- the accumulators are free after this;
+//   2. the next tile's first K-step operands are issued;
+//   3. the images leave as unconditional 16-B buffer stores (8 rows x 128 B per instruction);
+//   4. the next tile's first K-step waits only for its own loads (they are older than the
+//      stores: a counted vmcnt), so the stores drain under its MFMAs.
+// v2 (one tile per block) serialises per tile: the first operand loads' latency, the K loop,
+// the epilogue and the store drain before the block's slots free (t(K) = 0.83 ms + K 3.52 us
+// at N = 1152: the fixed part is the output at 4.5 TB/s, profiles/r04d_gemm_dma_ab_and_ksweep.txt).
+// The stores are raw buffer stores with out-of-range offsets instead of branches, and the
+// tile loop is rotated (epilogue first) with K-step 0 peeled out of the K loop: where paths
+// with different counts of younger memory operations merge, the compiler's waits count the
+// shortest and would wait for the stores.  bf16 output only (an fp32 tile needs 128 KB).
+constexpr int PP_LDS = 8 * 8192;   // operand tiles (48 KB) | 8 waves x two 4 KB row images
+
+// the thread index as a value the compiler cannot hoist out of (or keep across) the tile
+// loop: per-thread offsets are recomputed where they are used instead of holding VGPRs
+SM_DEV int opaque_tid() {
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+SM_DEV void bstore128(uint4 v, __amdgpu_buffer_rsrc_t rs, uint32_t off) {
+  __builtin_amdgcn_raw_buffer_store_b128(u32x4{v.x, v.y, v.z, v.w}, rs, off, 0, 0);
+}
+
+// descriptor over rows [0, rows_valid) of a row-major matrix (row_bytes apart) at base
+SM_DEV __amdgpu_buffer_rsrc_t rows_rsrc(const void* base, int64_t rows_valid, int64_t row_bytes) {
+  int64_t n = rows_valid > 0 ? rows_valid * row_bytes : 0;
+  if (n > (int64_t)BUF_OOB) n = BUF_OOB;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)n, 0x00020000);
+}
+
+// Epilogue math of one wave's 64 x 64 tile into its two 32-row images (img, img + 4096):
+// gemm_epilogue's VEC staged path for a bf16 output without aux / side outputs, with the
+// residual and bias reads as raw buffer loads (columns past N read zero).
+SM_DEV __attribute__((always_inline)) void pp_stage(const GemmArgs& g, const f32x16 (&acc)[2][2], int m0, int n0,
+                                                    int wm, int wn, int l, char* img) {
+  const int h = l >> 5;
+  const bool has_r = g.beta != 0.f;
+  const __bf16* Rsrc = g.R ? (const __bf16*)g.R : (const __bf16*)g.C;
+  const uint32_t s32 = seed32(g.seed), thr = drop_thr(g.drop_p);
+  const float ks = g.drop_p > 0.f ? 1.f / (1.f - g.drop_p) : 1.f;
+  const auto brs = __builtin_amdgcn_make_buffer_rsrc((void*)g.bias, (short)0, g.bias ? g.N * 4 : 0, 0x00020000);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const RowStage rs_{img + i * 4096};
+    const int r0 = m0 + wm + 32 * i;
+    const int row = r0 + (l & 31);
+    const float rsc = g.row_scale ? g.row_scale[(row < g.M ? row : g.M - 1) / (int)g.rows_per_group] : 1.f;
+    const uint32_t rb = drop_rowbase(s32, (uint64_t)row);
+    const auto rrs = rows_rsrc(Rsrc + (int64_t)r0 * g.ldc, (int64_t)g.M - r0, g.ldc * 2);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      uint4 rr[2];
+      if (has_r) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const int col = n0 + wn + 32 * j + 16 * p + 8 * h;
+          rr[p] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                rrs, col < g.N ? (uint32_t)(((l & 31) * g.ldc + col) * 2) : BUF_OOB, 0, 0));
+        }
+      }
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int col = n0 + wn + 32 * j + 16 * p + 8 * h;
+        float b8[8];
+        if (g.bias) {
+          const uint32_t o = col < g.N ? (uint32_t)col * 4u : BUF_OOB;
+          const float4 b0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(brs, o, 0, 0));
+          const float4 b1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(brs, o + 16, 0, 0));
+          b8[0] = b0.x; b8[1] = b0.y; b8[2] = b0.z; b8[3] = b0.w; b8[4] = b1.x; b8[5] = b1.y; b8[6] = b1.z; b8[7] = b1.w;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) b8[e] = 0.f;
+        }
+        // the run's 8 columns (v_permlane32_swap on copies: the accumulators stay intact)
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[i][j][8 * p + e]),
+                                                           __float_as_uint(acc[i][j][8 * p + 4 + e]), false, false);
+          v[e] = __uint_as_float(sw[0]);
+          v[4 + e] = __uint_as_float(sw[1]);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          v[e] = fmaf(v[e], g.alpha, b8[e]);
+          if (g.epi & 2) v[e] = (float)(__bf16)v[e];
+        }
+        if (g.epi & 1) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = gelu_f(v[e]);
+        }
+        if (g.drop_p > 0.f) {
+#pragma unroll
+          for (int e4 = 0; e4 < 8; e4 += 4) {
+            const uint32_t hv = drop_hash(rb, (uint32_t)(col + e4));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e4 + e] *= ((hv >> (8 * e)) & 0xFFu) >= thr ? ks : 0.f;
+          }
+        }
+        if (g.row_scale) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] *= rsc;
+        }
+        if (has_r) {
+          float r8[8];
+          load8((const __bf16*)&rr[p], r8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = fmaf(g.beta, r8[e], v[e]);
+        }
+        stage_put<__bf16>(rs_, 0, j, p, h, l, v);
+      }
+    }
+  }
+}
+
+// The wave's two images -> C by unconditional buffer stores (RowStage::flush's order and
+// statistics); rows past M are dropped by the descriptor, columns past N by the offset.
+template <bool STATS>
+SM_DEV __attribute__((always_inline)) void pp_flush(const GemmArgs& g, int m0, int n0, int wm, int wn, int l,
+                                                    const char* img) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's image writes
+  const int c = l & 7;
+  const int col = n0 + wn + 8 * c;
+  const bool cok = col < g.N;
+  float st1[8], st2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) st1[e] = st2[e] = 0.f;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r0 = m0 + wm + 32 * i;
+    const int rows_valid = g.M - r0;
+    const auto rs = rows_rsrc((const __bf16*)g.C + (int64_t)r0 * g.ldc, rows_valid, g.ldc * 2);
+    float a1[8], a2[8];
+    if constexpr (STATS) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a1[e] = a2[e] = 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = (l >> 3) + 8 * q;
+      const uint4 v = *(const uint4*)(img + i * 4096 + r * 128 + ((c ^ rs_swz(r)) << 4));
+      bstore128(v, rs, cok ? (uint32_t)((r * g.ldc + col) * 2) : BUF_OOB);
+      if constexpr (STATS) {
+        const bool in = cok && r < rows_valid;
+        const bf16x8 b = __builtin_bit_cast(bf16x8, v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float f = in ? (float)b[e] : 0.f;
+          a1[e] += f;
+          a2[e] = fmaf(f, f, a2[e]);
+        }
+      }
+    }
+    if constexpr (STATS) {   // the 8 row groups (l >> 3) of each chunk, fixed order (RowStage::flush)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+#pragma unroll
+        for (int x = 8; x < 64; x <<= 1) {
+          a1[e] += __shfl_xor(a1[e], x, 64);
+          a2[e] += __shfl_xor(a2[e], x, 64);
+        }
+        st1[e] += a1[e];
+        st2[e] += a2[e];
+      }
+    }
+  }
+  if constexpr (STATS) {   // this wave's 64 rows x 64 columns -> part row (m0 + wm) / 64, lanes 0..7
+    const int wrow = (m0 + wm) >> 6;
+    const int sc = n0 + wn + 8 * l;
+    const auto prs = __builtin_amdgcn_make_buffer_rsrc((void*)(g.stat_part + (int64_t)wrow * 2 * g.N), (short)0,
+                                                       2 * g.N * 4, 0x00020000);
+    const bool ok = l < 8 && m0 + wm < g.M && sc < g.N;
+    const uint32_t o = ok ? (uint32_t)sc * 4u : BUF_OOB;
+    const uint32_t o2 = ok ? (uint32_t)(g.N + sc) * 4u : BUF_OOB;
+    bstore128(make_uint4(__float_as_uint(st1[0]), __float_as_uint(st1[1]), __float_as_uint(st1[2]), __float_as_uint(st1[3])), prs, o);
+    bstore128(make_uint4(__float_as_uint(st1[4]), __float_as_uint(st1[5]), __float_as_uint(st1[6]), __float_as_uint(st1[7])), prs, o + 16);
+    bstore128(make_uint4(__float_as_uint(st2[0]), __float_as_uint(st2[1]), __float_as_uint(st2[2]), __float_as_uint(st2[3])), prs, o2);
+    bstore128(make_uint4(__float_as_uint(st2[4]), __float_as_uint(st2[5]), __float_as_uint(st2[6]), __float_as_uint(st2[7])), prs, o2 + 16);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+// K-major A; B K-major (forward, y = x W^T) or M/N-major (data gradient, dX = dy W); bf16
+// output; IMP 0 plain / 8 output BatchNorm statistics.  No split-K (k_begin = 0, k_chunk >=
+// K).  Grid: a multiple of 8 blocks, at most T / 8 per XCD group; block b serves group b & 7
+// (its tiles are a contiguous m-major range, so concurrently running blocks share A panels in
+// the XCD's L2) and walks tiles b >> 3, + gridDim.x / 8, ... of it.
+template <bool BK, int IMP>
+__global__ __launch_bounds__(512, 4) void gemm_bf16_pp(GemmArgs g) {
+  static_assert(IMP == 0 || IMP == 8, "persistent form: plain or statistics epilogue");
+  constexpr int BMV = 256, BNV = 128, NT = 512;
+  constexpr int CHA = TileLoader<BMV, NT, true>::CH, CHB = TileLoader<BNV, NT, BK>::CH;
+  constexpr int KSTEPB = TileLoader<BNV, NT, BK>::KSTEP;
+  __shared__ __attribute__((aligned(16))) char lds[PP_LDS];
+  char* la = lds;
+  char* lb = lds + BMV * BKT * 2;
+  // the wave index in a scalar register: the epilogue's descriptors hang off it
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  char* img = lds + w * 8192;
+  const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
+  const int ntn = (g.N + BNV - 1) / BNV;
+  const int T = ntn * ((g.M + BMV - 1) / BMV);
+  const int x = blockIdx.x & 7, qstep = gridDim.x >> 3;
+  const int T8 = T >> 3, R8 = T & 7;
+  const int cnt = T8 + (x < R8 ? 1 : 0), tbase = x * T8 + (x < R8 ? x : R8);
+  const int it = blockIdx.x >> 3;
+  if (it >= cnt) return;
+  const __bf16* A = (const __bf16*)g.A;
+  const __bf16* B = (const __bf16*)g.B;
+  const int K = g.K;
+  const int nk = (K + BKT - 1) / BKT;
+  const uint32_t a_rs = (uint32_t)((NT / 8) * g.lda * 2);   // bytes between a thread's chunks
+  const uint32_t b_rs = BK ? (uint32_t)((NT / 8) * g.ldb * 2) : (uint32_t)(KSTEPB * g.ldb * 2);
+
+  int lm0 = 0, ln0 = 0;   // the loaders' tile
+  auto setup = [&](int i) {
+    const int tt = tbase + i;
+    lm0 = (tt / ntn) * BMV;
+    ln0 = (tt % ntn) * BNV;
+  };
+  // operand staging (TileLoader's chunk map; rows past the matrix clipped by the descriptor's
+  // record count (K-major) or an out-of-range offset (M/N-major columns), chunks past K by
+  // the K check; the per-chunk stride is the scalar offset)
+  uint4 ra[CHA], rb[CHB];
+  auto issue = [&](int k0) {
+    const int t = opaque_tid();
+    const int kv = K - k0;
+    const int arows = g.M - lm0 < BMV ? g.M - lm0 : BMV;
+    const auto rsa = __builtin_amdgcn_make_buffer_rsrc((void*)(A + (int64_t)lm0 * g.lda + k0), (short)0,
+                                                       (int)(((int64_t)arows * g.lda - k0) * 2), 0x00020000);
+    const int kk = (t & 7) * 8;
+    const uint32_t a_v = kk < kv ? (uint32_t)(((t >> 3) * g.lda + kk) * 2) : BUF_OOB;
+#pragma unroll
+    for (int i = 0; i < CHA; ++i)
+      ra[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsa, a_v, i * a_rs, 0));
+    const int bcols = g.N - ln0 < BNV ? g.N - ln0 : BNV;
+    if constexpr (BK) {
+      const auto rsb = __builtin_amdgcn_make_buffer_rsrc((void*)(B + (int64_t)ln0 * g.ldb + k0), (short)0,
+                                                         (int)(((int64_t)bcols * g.ldb - k0) * 2), 0x00020000);
+      const uint32_t b_v = kk < kv ? (uint32_t)(((t >> 3) * g.ldb + kk) * 2) : BUF_OOB;
+#pragma unroll
+      for (int i = 0; i < CHB; ++i)
+        rb[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsb, b_v, i * b_rs, 0));
+    } else {
+      const auto rsb = panel_rsrc(B, (int64_t)k0 * g.ldb + ln0);
+      const int bk = t / (BNV / 8), bc = (t % (BNV / 8)) * 8;
+      const uint32_t b_v = (uint32_t)((bk * g.ldb + bc) * 2);
+#pragma unroll
+      for (int i = 0; i < CHB; ++i)
+        rb[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              rsb, (bc < bcols && bk + KSTEPB * i < kv) ? b_v : BUF_OOB, i * b_rs, 0));
+    }
+  };
+  auto put = [&]() {
+    const int t = opaque_tid();
+    const int a_l0 = kmaj_off(t >> 3, t & 7);
+    const int b_l0 = BK ? a_l0 : mnmaj_off_r<BNV>(t / (BNV / 8), (t % (BNV / 8)) * 8);
+#pragma unroll
+    for (int i = 0; i < CHA; ++i) *(uint4*)(la + a_l0 + i * TileLoader<BMV, NT, true>::LSTEP) = ra[i];
+#pragma unroll
+    for (int i = 0; i < CHB; ++i) *(uint4*)(lb + b_l0 + i * TileLoader<BNV, NT, BK>::LSTEP) = rb[i];
+  };
+  f32x16 acc[2][2];
+  auto kstep = [&]() {
+#pragma unroll
+    for (int s = 0; s < BKT / 16; ++s) {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = lread_frag_r<true, BMV>(la, wm + 32 * i, s);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfr[j] = lread_frag_r<BK, BNV>(lb, wn + 32 * j, s);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      // v2's order: the substep's four fragment reads, then its four MFMAs (left to itself the
+      // scheduler here issued the fourth read behind two MFMAs and waited on it)
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    }
+  };
+  // the K loop of the loaders' tile, its K-step 0 operands already issued
+  auto ksteps = [&]() {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    put();   // K-step 0, outside the loop (see above)
+    __syncthreads();
+    if (nk > 1) issue(BKT);
+    kstep();
+    __syncthreads();
+    for (int ks = 1; ks < nk; ++ks) {
+      put();
+      __syncthreads();
+      if (ks + 1 < nk) issue((ks + 1) * BKT);
+      kstep();
+      __syncthreads();
+    }
+  };
+  setup(it);
+  issue(0);
+  ksteps();
+  int cm0 = lm0, cn0 = ln0;
+  for (int in = it + qstep; in < cnt; in += qstep) {
+    pp_stage(g, acc, cm0, cn0, wm, wn, opaque_tid() & 63, img);
+    setup(in);
+    issue(0);
+    pp_flush<IMP == 8>(g, cm0, cn0, wm, wn, opaque_tid() & 63, img);
+    __syncthreads();   // every wave's images read before the next tile's operands land
+    cm0 = lm0;
+    cn0 = ln0;
+    ksteps();
+  }
+  pp_stage(g, acc, cm0, cn0, wm, wn, threadIdx.x & 63, img);
+  pp_flush<IMP == 8>(g, cm0, cn0, wm, wn, threadIdx.x & 63, img);
+}
+
 // ============================================================ f32 MFMA kernel
 constexpr int FBM = 64, FBN = 64, FBK = 16, FLD = 64 + 4;
 
@@ -1131,11 +1460,9 @@ int choose_splits(int M, int N, int K, bool bf16) {
   const int64_t tiles = (int64_t)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   const int64_t slots = bf16 ? gemm_slots(v) : 512;
   if (tiles >= slots || K < 4096) return 1;
-  static const int rounds = [] {   // SM_GEMM_SPLIT_ROUNDS pins the round count (A/B runs)
-    const char* e = getenv("SM_GEMM_SPLIT_ROUNDS");
-    const int x = e ? atoi(e) : 0;
-    return (x >= 1 && x <= 64) ? x : 2;
-  }();
+  // two rounds: 2-16 rounds measured the same time (profiles/r04f_dw_rounds.txt; the A/B knob
+  // that pinned the count, and so the reduction order, is gone: results stay reproducible)
+  constexpr int rounds = 2;
   int64_t want = bf16 ? (rounds * slots) / tiles : (1024 + tiles - 1) / tiles;
   int64_t max_by_k = K / (4 * bk);
   int64_t s = want < max_by_k ? want : max_by_k;
@@ -1171,11 +1498,56 @@ int gemm_variant(int M, int N, int K) {
 int variant_bm(int v) { return v == 2 ? 256 : 128; }
 int variant_bn(int v) { return 128; (void)v; }
 
+// Persistent pipelined form (gemm_bf16_pp) for a non-split bf16 GEMM with a K-major A at
+// BM = 256 whose epilogue has no side output: used when the grid would take more than one
+// round of resident blocks.  sm_gemm_persistent(0) (or SM_GEMM_PP=0 at process start) selects
+// the one-tile-per-block v2 form; both give bit-identical outputs.
+int pp_mode = -1;   // -1: not yet read from the environment
+bool pp_enabled() {
+  if (pp_mode < 0) {
+    const char* e = getenv("SM_GEMM_PP");
+    pp_mode = (e && e[0] == '0') ? 0 : 1;
+  }
+  return pp_mode != 0;
+}
+// K <= 128 only: same-box A/B (profiles/r05b_gemm_persistent_ab.txt) -- the write-bound small-K
+// shapes gain 4-13 % (stage-0 expand 7.40 -> 6.46 ms, its BatchNorm-input data gradient 7.00 ->
+// 6.71), K = 256 / 384 are even, K = 768 / 1536 lose 9 %: persistent blocks drift apart, so the
+// n-tile blocks that share an A panel no longer stream it through L2 together.
+bool pp_ok(const GemmArgs& g) {
+  return pp_enabled() && g.partial == nullptr && g.colsum == nullptr && !g.ctrans && !(g.epi & 4) &&
+         !((g.epi & 1) && g.aux) && g.aux_out == nullptr && g.K > 0 && g.K <= 2 * BKT && g.k_begin == 0 &&
+         g.k_chunk >= g.K;
+}
+template <bool BK, int IMP>
+bool launch_pp(const GemmArgs& g, hipStream_t st) {
+  static int slots = 0;   // resident blocks on the device, a multiple of 8 (occupancy query, cached)
+  if (slots == 0) {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, gemm_bf16_pp<BK, IMP>, 512, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      cus = 256;
+      per = 2;
+    }
+    slots = (cus * (per > 0 ? per : 1)) & ~7;
+    if (slots < 8) slots = 8;
+  }
+  const int64_t tiles = (int64_t)((g.N + 127) / 128) * ((g.M + 255) / 256);
+  if (tiles <= slots) return false;   // one round: the one-tile-per-block form
+  hipLaunchKernelGGL((gemm_bf16_pp<BK, IMP>), dim3(slots), dim3(512), 0, st, g);
+  return true;
+}
+
 template <bool AK, bool BK, typename TC, bool VEC>
 void launch_bf16(const GemmArgs& g, int splits, hipStream_t st) {
   const int v = gemm_variant(g.M, g.N, g.K);
   const int bm = variant_bm(v), bn = variant_bn(v);
   const int tiles = ((g.N + bn - 1) / bn) * ((g.M + bm - 1) / bm);
+  if constexpr (AK && VEC && sizeof(TC) == 2) {
+    if (v == 2 && splits == 1 && pp_ok(g) && launch_pp<BK, 0>(g, st)) return;
+  }
   if (v == 1) hipLaunchKernelGGL((gemm_bf16_kernel<AK, BK, TC, VEC>), dim3(tiles, 1, splits), dim3(256), 0, st, g);
   else if (v == 2) hipLaunchKernelGGL((gemm_bf16_v2<AK, BK, TC, VEC, 256>), dim3(tiles * splits), dim3(512), 0, st, g);
   else hipLaunchKernelGGL((gemm_bf16_v2<AK, BK, TC, VEC, 128>), dim3(tiles * splits), dim3(256), 0, st, g);
@@ -1294,6 +1666,12 @@ extern "C" int sm_conv3x3_wgrad(const void* dy, const void* x, float* dw, int ac
     SM_CHECK_LAUNCH();
   }
   return 0;
+}
+
+extern "C" int sm_gemm_persistent(int mode) {
+  const int prev = pp_enabled() ? 1 : 0;
+  if (mode >= 0) pp_mode = mode ? 1 : 0;
+  return prev;
 }
 
 extern "C" int64_t sm_gemm_workspace_bytes(int ab_dtype, int M, int N, int K) {
@@ -1553,7 +1931,8 @@ extern "C" int sm_linear_bn_stats(int M, int N, int K, const void* x, const void
   g.alpha = 1.f; g.beta = 0.f; g.rows_per_group = 1; g.k_begin = 0; g.k_chunk = K;
   g.stat_part = part;
   const int tiles_n = (N + 127) / 128;
-  if (gemm_variant(M, N, K) == 2)
+  if (gemm_variant(M, N, K) == 2 && pp_ok(g) && launch_pp<true, 8>(g, stream)) {
+  } else if (gemm_variant(M, N, K) == 2)
     hipLaunchKernelGGL((gemm_bf16_v2<true, true, __bf16, true, 256, 8>), dim3(tiles_n * ((M + 255) / 256)), dim3(512),
                        0, stream, g);
   else

@@ -23,6 +23,7 @@ _c_p = ctypes.c_void_p
 # name -> (restype, argtypes)
 _SIGS = {
     "sm_gemm_workspace_bytes": (_c_i64, [_c_i32, _c_i32, _c_i32, _c_i32]),
+    "sm_gemm_persistent": (_c_i32, [_c_i32]),
     "sm_gemm": (_c_i32, [_c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_i64, _c_p, _c_i64,
                          _c_p, _c_i64, _c_p, _c_f32, _c_f32, _c_i32, _c_p, _c_p, _c_f32, _c_u64, _c_p, _c_i64,
                          _c_p, _c_i64, _c_p]),

@@ -39,6 +39,12 @@ def gemm(A, B, C, M, N, K, a_layout, b_layout, lda, ldb, ldc, bias=None, alpha=1
     return C
 
 
+def gemm_persistent(mode=-1):
+    """Select the persistent (1) or one-tile-per-block (0) form of the plain bf16 forward /
+    data-gradient GEMMs (bit-identical outputs); mode < 0 queries.  Returns the previous mode."""
+    return int(query("sm_gemm_persistent", int(mode)))
+
+
 def linear(x, w, bias=None, out_dtype=None, gelu=False, residual=None, round_branch=False, drop_p=0.0, seed=0,
            row_scale=None, rows_per_group=1):
     """y = residual + rs[row] * drop(act(x @ w^T + bias)); returns (y, pre-activation) with GELU."""

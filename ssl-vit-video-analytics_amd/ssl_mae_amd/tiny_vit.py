@@ -105,15 +105,16 @@ class PatchEmbed(nn.Module):
     # training): False keeps the stored y = BN2(a2) (bit-identical either way)
     fold_bn2 = True
 
-    def run(self, clip, mode):
+    def run(self, clip, mode, fold_ok=True):
         """-> (t, x_bn): t the stem output, or with x_bn = (mean, rstd, weight, bias) of BN2
-        the conv2 output a2 that stages[0][0] reads as bf16(BN2(a2)) (StemFn)."""
+        the conv2 output a2 that stages[0][0] reads as bf16(BN2(a2)) (StemFn).  fold_ok: the
+        consumer can take the folded form (TinyViT._stem_fold_ok)."""
         pe = self.patch_embed
         if pe[0].c.weight.shape[:2] != (48, 3) or pe[2].c.weight.shape[:2] != (96, 48):
             raise NotImplementedError("fused stem is specialised for 3->48->96 (embed_dims[0]=96)")
         bn1, bn2 = pe[0].bn, pe[2].bn
         wo = (clip.shape[-1] - 1) // 2 + 1
-        fold = bool(self.fold_bn2) and mode.bf16 and bn1.training and bn2.training and wo <= 128
+        fold = bool(self.fold_bn2) and fold_ok and mode.bf16 and bn1.training and bn2.training and wo <= 128
         st = _St(mode=mode, bn1=bn1, bn2=bn2, fold_bn2=fold)
         t, m2, r2 = StemFn.apply(clip, st, pe[0].c.weight, bn1.weight, bn1.bias, pe[2].c.weight, bn2.weight,
                                  bn2.bias)
@@ -259,9 +260,16 @@ class TinyViT(nn.Module):
                 x = stage.run(x, mode, False, xb)
         return x
 
+    def _stem_fold_ok(self):
+        """The stem's BN2 fold needs a consumer that forms bf16(BN2(a2)) in its loads: a fused
+        MBConv first block (the BatchNorm-input expand GEMM: mid % 32 == 0, <= 256 input
+        channels); anything else takes the stem's stored output."""
+        blk = self.stages[0][0] if len(self.stages[0]) else None
+        return isinstance(blk, MBConv) and blk.mid % 32 == 0 and blk.in_chans <= 256
+
     def tokens_stage3(self, clip, mode):
         """clip [B,3,T,H,W] or frames [N,3,H,W] -> channels-last [N*T, H/8, W/8, 384]."""
-        x, x_bn = self.patch_embed.run(clip, mode)
+        x, x_bn = self.patch_embed.run(clip, mode, self._stem_fold_ok())
         return self._run_stages(x, 3, mode, x_bn)
 
     def _prepare(self, mode):
@@ -279,7 +287,7 @@ class TinyViT(nn.Module):
     def tokens_all(self, x, mode):
         """All four stages, channels-last: frames [N,3,H,W] (any strides) or a clip
         [B,3,T,H,W] (frames b*T + t) -> [N, H/16, W/16, C4]."""
-        t, x_bn = self.patch_embed.run(x, mode)
+        t, x_bn = self.patch_embed.run(x, mode, self._stem_fold_ok())
         return self._run_stages(t, 4, mode, x_bn)
 
     def forward(self, x):

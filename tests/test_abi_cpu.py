@@ -47,7 +47,8 @@ def test_torch_library_registration():
              "scale": "scale_", "dwconv_fused_fwd": "dwconv_fused", "pos_blend_fwd": "pos_blend",
              "dwconv_s2_bn_bwd": "dwconv_bn_bwd"}   # ssl_mae::dwconv_bn_bwd dispatches on stride
     internal = {"add",                       # not used by the step
-                "bn_stats_from_partials"}    # the statistics step inside ssl_mae::dwconv_fused
+                "bn_stats_from_partials",    # the statistics step inside ssl_mae::dwconv_fused
+                "gemm_persistent"}           # a host-side mode switch, no compute
     for sym in _lib.exported_symbols():
         base = sym[3:]
         if base.endswith(("_workspace_bytes", "_partial_rows")) or base in internal:

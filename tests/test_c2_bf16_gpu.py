@@ -383,7 +383,10 @@ def test_bf16_full_c2_step_properties():
         assert abs(loss.item() - ref) < 1e-4 * abs(ref), (loss.item(), ref)
         del x, tgt, m, per_tok
     assert all(math.isfinite(v) for v in losses)
-    assert 1.0 < losses[0] < 3.0, losses
+    # model-level anchor (the formula check above only validates the loss kernel): the first-step
+    # loss of the set_seed(42)-style init on uniform clips, against the reference-run golden's
+    # B = 1 value 1.979 (tests/golden, step_b1_t8_s224); 15 % covers the batch's sampling spread
+    assert abs(losses[0] - 1.979) < 0.15 * 1.979, losses
     assert idx.numel() == B_BENCH * T_BENCH * 588
     assert not torch.equal(p0, model.decoder_pred.weight)
     for name, b in model.named_buffers():

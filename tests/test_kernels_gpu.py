@@ -840,6 +840,62 @@ def test_linear_dw_se_operand(Fr, HW, N, C, acc):
         assert rel_err(h3.float(), hh) < 1e-2
 
 
+@pytest.mark.parametrize("case", ["bias", "bias_unaligned", "gelu", "branch", "dx", "dx_res", "k128", "k40",
+                                  "stats"])
+def test_gemm_persistent_bit_identical(case):
+    """The persistent GEMM form (gemm_bf16_pp: tile epilogues written through LDS and stored
+    under the next tile's K loop; K <= 128) against the one-tile-per-block v2 form, bit for
+    bit: ragged M (a partial last m-tile) and N (392: a partial n-tile), K tails (96, 40: one
+    K-step), every epilogue option of the plain form (bias, GELU without side output, the
+    autocast-rounded branch + dropout + DropPath + residual), the data-gradient layout
+    (M/N-major B), and the BatchNorm-statistics epilogue.  > 512 tiles: the persistent path."""
+    kk = KK()
+    M, N, Kd = 256 * 200 + 77, 392, 96
+    if case == "k128":
+        Kd = 128
+    elif case == "k40":
+        Kd = 40
+    elif case == "stats":
+        M, N = 256 * 300 + 13, 384
+    x = rnd(M, Kd, dtype=torch.bfloat16, seed=310).to(DEV)
+    w = rnd(N, Kd, dtype=torch.bfloat16, seed=311, scale=0.2).to(DEV)
+    bias_buf = rnd(N + 1, seed=312).to(DEV)
+    bias = bias_buf[1:] if case == "bias_unaligned" else bias_buf[:N]
+    res = rnd(M, N, dtype=torch.bfloat16, seed=313).to(DEV)
+    rs = (torch.rand(64, generator=torch.Generator().manual_seed(314)) * 2).to(DEV)
+
+    def run():
+        if case in ("dx", "dx_res"):   # dX[M][Kd'] = dy[M][N] w[N][Kd']: here dy = x, w' = [Kd][N']
+            wt = rnd(Kd, 264, dtype=torch.bfloat16, seed=315, scale=0.2).to(DEV)
+            r2 = rnd(M, 264, dtype=torch.bfloat16, seed=316).to(DEV) if case == "dx_res" else None
+            return (kk.linear_dx(x, wt, residual=r2),)
+        if case == "stats":
+            rm, rv = torch.zeros(N, device=DEV), torch.ones(N, device=DEV)
+            nb = torch.zeros((), dtype=torch.int64, device=DEV)
+            return kk.linear_bn_stats(x, w, rm, rv, 0.1, 1e-5, 1, nb) + (rm, rv)
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        if case == "gelu":
+            kk.gemm(x, w, out, M, N, Kd, 0, 0, Kd, Kd, N, bias=bias, gelu=True)
+        elif case == "branch":
+            kk.gemm(x, w, out, M, N, Kd, 0, 0, Kd, Kd, N, bias=bias, beta=1.0, R=res, round_branch=True,
+                    drop_p=0.1, seed=77, row_scale=rs, rows_per_group=M // 63)
+        else:
+            kk.gemm(x, w, out, M, N, Kd, 0, 0, Kd, Kd, N, bias=bias)
+        return (out,)
+
+    prev = kk.gemm_persistent(0)
+    try:
+        ref = run()
+        kk.gemm_persistent(1)
+        got = run()
+    finally:
+        kk.gemm_persistent(prev)
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b), case
+    if case == "bias":
+        assert rel_err(got[0], x.float() @ w.float().t() + bias) < TOL[torch.bfloat16]
+
+
 @pytest.mark.parametrize("M,N,Kd,upd", [(100000, 384, 96, 2), (1000, 384, 96, 1), (100, 96, 64, 1), (4097, 40, 32, 2),
                                         (12544 * 32, 384, 96, 2), (12544 * 32 + 77, 384, 96, 1),
                                         (12544 * 32, 384, 64, 1)])
