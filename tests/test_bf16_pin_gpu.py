@@ -9,17 +9,22 @@ fp32 steps (tests/test_model_gpu.py).  The benchmarked bf16 kernels are pinned h
      mask): the bf16 model's stem output, stage 0/1/2 outputs and pred against the fp32
      CPU oracle's (itself checked against the reference's golden activation sums), by
      relative L2 error (||a - b|| / ||b||) and relative max error (max|a - b| / max|b|).
-     Tolerances, 2x the measured errors (profiles/r04d_bf16_pin_probe.txt: 5.0e-3, 8.9e-3,
-     1.4e-2, 1.9e-2, 1.2e-2 rel L2):
-        stem 1e-2 | stage0 2e-2 | stage1 3e-2 | stage2 4e-2 | pred 3e-2   (rel L2)
-        stem 1.5e-2 | stage0 2e-2 | stage1 3e-2 | stage2 4e-2 | pred 5e-2 (rel max)
+     Tolerances: 1.5x what the REFERENCE's own bf16 autocast run lands from its own fp32
+     run on the same clip, mask and weights (tests/golden/bf16_anchor_b1_t8_s224.npz, made
+     by tests/golden/make_golden_bf16.py: rel L2 5.4e-3 / 1.04e-2 / 1.62e-2 / 2.28e-2 /
+     1.24e-2, rel max 6.3e-3 / 1.08e-2 / 1.71e-2 / 2.41e-2 / 2.45e-2 for stem / stage 0-2 /
+     pred); this build measured 5.0e-3 / 8.9e-3 / 1.4e-2 / 1.9e-2 / 1.2e-2 rel L2
+     (profiles/r04d_bf16_pin_probe.txt), i.e. at or below the reference's own bf16 error.
   2. a whole bf16 training step at B=32, T=8, 224^2 (dropout and DropPath ON: both modes
      draw the same counter-hash masks) against the fp32-mode HIP step on the same clips and
      mask: loss within 0.1 % (measured 1e-4 at B=16), every parameter gradient with
      cosine > 0.98 and norm within 5 %, 95 % of them with cosine > 0.995, and the
      concatenated gradient cosine > 0.999.  Gradients that are zero analytically (biases
      whose output only feeds a train-mode BatchNorm, e.g. the stem BN2 bias) are skipped:
-     their fp32 norm is rounding noise (< 1e-5 of the largest).
+     their fp32 norm is rounding noise (< 1e-5 of the largest).  For scale: the reference's
+     own bf16 autocast step at B=1 against its fp32 step (the anchor fixture) has loss
+     within 4.7e-4, a concatenated gradient cosine of 0.99987 and a 5th-percentile
+     per-parameter cosine of 0.9936 (minimum 0.41, one near-zero gradient).
 """
 import math
 import os
@@ -31,8 +36,13 @@ import torch
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
-STAGE_TOL = {"act_stem": (1e-2, 1.5e-2), "act_stage0": (2e-2, 2e-2), "act_stage1": (3e-2, 3e-2),
-             "act_stage2": (4e-2, 4e-2), "pred": (3e-2, 5e-2)}
+STAGE_KEYS = ("act_stem", "act_stage0", "act_stage1", "act_stage2", "pred")
+ANCHOR_X = 1.5   # tolerance = 1.5x the reference's own bf16-vs-fp32 error
+
+
+def _stage_tol(golden_dir):
+    a = np.load(os.path.join(golden_dir, "bf16_anchor_b1_t8_s224.npz"))
+    return {k: (ANCHOR_X * float(a["rel_l2/" + k]), ANCHOR_X * float(a["rel_max/" + k])) for k in STAGE_KEYS}
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -106,7 +116,7 @@ def test_bf16_stage_outputs_vs_oracle_c2_clip(golden_dir):
     acts = {}
     with torch.no_grad():
         O.mae_forward(P, clip.cpu(), mask.cpu(), cfg, None, acts)
-    for k, (tl2, tmax) in STAGE_TOL.items():
+    for k, (tl2, tmax) in _stage_tol(golden_dir).items():
         ref = acts[k].float()
         if k + "_sumsq" in d.files:   # the oracle run is the reference's (golden activation sums)
             assert abs(float((ref.double() ** 2).sum()) / float(d[k + "_sumsq"]) - 1) < 1e-4, k

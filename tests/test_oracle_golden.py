@@ -155,3 +155,18 @@ def test_reference_init_under_seed42(golden_dir):
         v = p.detach().double().numpy().ravel()
         assert np.array_equal(v[:8].astype(np.float32), d["head/" + n]), n
         assert v.sum() == float(d["sum/" + n]) and (v * v).sum() == float(d["sumsq/" + n]), n
+
+
+def test_bf16_anchor_fixture(golden_dir):
+    """tests/golden/bf16_anchor_b1_t8_s224.npz (make_golden_bf16.py: the reference's own bf16
+    autocast run against its own fp32 run) is the same fp32 run as the step_b1_t8_s224 golden
+    (bit-equal loss), and its per-stage errors are bf16-sized and grow with depth through the
+    encoder -- the scale test_bf16_pin_gpu.py gates the timed bf16 kernels at (1.5x)."""
+    a = np.load(os.path.join(golden_dir, "bf16_anchor_b1_t8_s224.npz"))
+    d = np.load(os.path.join(golden_dir, "step_b1_t8_s224.npz"))
+    assert float(a["loss_fp32"]) == float(d["avg_loss"])
+    assert abs(float(a["loss_bf16"]) / float(a["loss_fp32"]) - 1) < 1e-2
+    l2 = [float(a["rel_l2/" + k]) for k in ("act_stem", "act_stage0", "act_stage1", "act_stage2")]
+    assert all(1e-3 < e < 5e-2 for e in l2) and l2 == sorted(l2)
+    assert 1e-3 < float(a["rel_l2/pred"]) < 5e-2
+    assert float(a["grad_cos_all"]) > 0.999 and len(a["grad_names"]) == len(a["grad_cos"]) > 150
