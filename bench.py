@@ -62,15 +62,19 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(T, S, ratio, B=4):
+def cpu_baseline(T, S, ratio, B=1):
     """The CPU oracle (fp32 restatement of the reference path) timed on the host
-    cores at BASELINE config 1's batch: one fwd+bwd+AdamW step of B = 4 clips (the
-    reference's C1 step, train_ssl_mae.py:66-91; bounded sample, ~30 s)."""
+    cores: one fwd+bwd+AdamW step of the reference's C1 step (train_ssl_mae.py:66-91,
+    T=8, 224^2) on B = 1 clip (a bounded sample: the reference's own C1 batch of 4 takes
+    ~2 min on 8 cores), with dropout / DropPath on as the reference ships them (attention
+    probabilities materialised per head, as nn.MultiheadAttention's math path), after an
+    untimed small warm-up step (thread pool, allocator); torch's threads = the box's CPU
+    share (OMP_NUM_THREADS).  ~20-40 s."""
     from oracle import mae_oracle as O
     from ssl_mae_amd.init_rule import param_value, synthetic_clip
     cfg = {"dataset": {"clip_len": T, "image_size": S},
            "model": {"decoder_embed_dim": 384, "decoder_depth": 4, "decoder_num_heads": 6},
-           "ssl": {"mask_ratio": ratio, "norm_pix_loss": True}}
+           "ssl": {"mask_ratio": ratio, "norm_pix_loss": True}, "train_dropout": True}
     threads = torch.get_num_threads()
     try:
         affinity = len(os.sched_getaffinity(0))
@@ -79,17 +83,23 @@ def cpu_baseline(T, S, ratio, B=4):
     P = O.make_params(cfg, param_value)
     bufs = O.init_buffers(P)
     opt = O.AdamWState(lr=5e-4)
-    clip = torch.from_numpy(synthetic_clip(B, T, S, seed=7))
     torch.manual_seed(42)
+    wcfg = dict(cfg, dataset={"clip_len": 2, "image_size": 64})
+    wP = O.make_params(wcfg, param_value)
+    O.train_step(wP, O.init_buffers(wP), O.AdamWState(lr=5e-4), torch.from_numpy(synthetic_clip(1, 2, 64, seed=6)),
+                 O.get_tube_mask(1, 2, 64, ratio), wcfg)   # warm-up (small)
+    del wP
+    clip = torch.from_numpy(synthetic_clip(B, T, S, seed=7))
     mask = O.get_tube_mask(B, T, (S // 8) ** 2, ratio)
     t0 = time.perf_counter()
     O.train_step(P, bufs, opt, clip, mask, cfg)
     dt = time.perf_counter() - t0
     return {"value": round(B / dt, 5), "unit": "clips/s", "cores": threads, "threads": threads,
             "nproc": os.cpu_count(), "affinity_cpus": affinity, "kind": "port",
-            "sample": f"BASELINE config 1 step: {B} clips {T}x3x{S}x{S}, one fp32 fwd+bwd+AdamW step of "
-                      f"oracle/mae_oracle.py (dropout off) on {threads} torch threads (nproc {os.cpu_count()}, "
-                      f"affinity {affinity}); {dt:.1f} s"}
+            "sample": f"BASELINE config 1 step shape on {B} clip ({T}x3x{S}x{S}): one fp32 fwd+bwd+AdamW step of "
+                      f"oracle/mae_oracle.py with dropout / DropPath on (as the reference), after a small "
+                      f"warm-up step, on {threads} torch threads (the box's CPU share; nproc "
+                      f"{os.cpu_count()}, affinity {affinity}); {dt:.1f} s"}
 
 
 PROBE_KERNELS = {"dec_attn_fwd": "attn_fwd_bf16<64, true>",
@@ -262,9 +272,11 @@ def main():
     probe.active = True
     stem_probe.active = True
     t0 = time.perf_counter()
-    losses = []
+    loss_vals = []
     for i in range(args.steps):
-        losses.append(step(i))
+        # the reference syncs on the loss every step (total_loss += loss.item(),
+        # train_ssl_mae.py:91): so does the timed loop
+        loss_vals.append(float(step(i).item()))
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     probe.active = False
@@ -276,7 +288,6 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-    loss_vals = [float(l.item()) for l in losses]
     peak_mem = torch.cuda.max_memory_allocated(dev) / 2 ** 30
 
     if rank == 0:
@@ -335,6 +346,7 @@ def main():
             "model_mfu": round(step_tflops / MFMA_BF16_PEAK_TFLOPS, 4) if step_tflops else None,
             "peak_mem_gib": round(peak_mem, 1),
             "loss_first_last": [round(loss_vals[0], 5), round(loss_vals[-1], 5)],
+            "loss_item_per_step": True,
             "cpu_baseline": cpu,
             "cpu_baseline_reference": reference_cpu() if not small else None,
         }

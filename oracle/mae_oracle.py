@@ -26,7 +26,13 @@ What it follows (reference file:line, relative to the reference repo root):
                          built at src/models/mae_vit_adapter.py:40-48
   AdamW step             src/train_ssl_mae.py:163 (lr from config, wd 0.05, betas
                          (0.9, 0.999), eps 1e-8; params whose grad is None skipped)
-Dropout / DropPath are 0 in parity mode.
+Dropout / DropPath are 0 in parity mode.  cfg["train_dropout"] = True
+(bench.py's cpu_baseline only, never a parity check) runs them as the reference ships them,
+on torch's CPU RNG: the decoder layers' nn.Dropout(0.1) on the attention probabilities, the
+attention output, the FF activation and the FF output (torch TransformerEncoderLayer
+defaults), and the encoder blocks' DropPath with rates linspace(0, 0.1, 12)
+(tiny_vit.py:146-158, timm's per-sample stochastic depth) -- the reference's CPU step
+spends ~41 % of its time in those bernoulli draws.
 """
 import math
 
@@ -105,14 +111,29 @@ def _se(P, pre, x):
     return x * s[:, :, None, None]
 
 
-def _mbconv(P, pre, x, cin, cout, stride, trk, upd):
+_DROP = {"on": False}
+
+
+def _drop_path(h, p):
+    """timm DropPath (scale_by_keep): per-sample keep with prob 1 - p, kept rows / (1 - p)."""
+    if not _DROP["on"] or p <= 0.0:
+        return h
+    keep = torch.empty((h.shape[0],) + (1,) * (h.dim() - 1)).bernoulli_(1 - p)
+    return h * keep / (1 - p)
+
+
+def _dropout(x, p=0.1):
+    return F.dropout(x, p, training=True) if _DROP["on"] else x
+
+
+def _mbconv(P, pre, x, cin, cout, stride, trk, upd, dp=0.0):
     mid = cin * 4
     h = F.gelu(_conv_bn(P, pre + ".conv.0", x, trk=trk, updates=upd))
     h = F.gelu(_conv_bn(P, pre + ".conv.2", h, stride, 1, mid, trk=trk, updates=upd))
     h = _se(P, pre + ".conv.4", h)
     h = _conv_bn(P, pre + ".conv.5", h, trk=trk, updates=upd)
     if stride == 1 and cin == cout:
-        return x + h
+        return x + _drop_path(h, dp)
     return h
 
 
@@ -125,7 +146,7 @@ def _attention_core(q, k, v):
     return F.scaled_dot_product_attention(q, k, v)
 
 
-def _vit_block(P, pre, x, heads):
+def _vit_block(P, pre, x, heads, dp=0.0):
     N, C, H, W = x.shape
     t = x.flatten(2).transpose(1, 2)
     d = C // heads
@@ -133,15 +154,17 @@ def _vit_block(P, pre, x, heads):
     qkv = h @ P[pre + ".attn.qkv.weight"].t() + P[pre + ".attn.qkv.bias"]
     qkv = qkv.reshape(N, H * W, 3, heads, d).permute(2, 0, 3, 1, 4)
     a = _attention_core(qkv[0], qkv[1], qkv[2]).transpose(1, 2).reshape(N, H * W, C)
-    t = t + (a @ P[pre + ".attn.proj.weight"].t() + P[pre + ".attn.proj.bias"])
+    t = t + _drop_path(a @ P[pre + ".attn.proj.weight"].t() + P[pre + ".attn.proj.bias"], dp)
     h = _ln(P, pre + ".norm2", t)
     h = F.gelu(h @ P[pre + ".mlp.fc1.weight"].t() + P[pre + ".mlp.fc1.bias"])
-    t = t + (h @ P[pre + ".mlp.fc2.weight"].t() + P[pre + ".mlp.fc2.bias"])
+    t = t + _drop_path(h @ P[pre + ".mlp.fc2.weight"].t() + P[pre + ".mlp.fc2.bias"], dp)
     return t.transpose(1, 2).reshape(N, C, H, W)
 
 
 def forward_stage3(P, x, trk=None, prefix="encoder.", acts=None, depths=DEPTHS):
     pe = prefix + "patch_embed.patch_embed"
+    dpr = torch.linspace(0, 0.1, sum(depths)).tolist()   # TinyViT drop_path_rate 0.1 (tiny_vit.py:146)
+    cur = 0
     h = F.gelu(_conv_bn(P, pe + ".0", x, 2, 1, trk=trk, updates=1))
     h = _conv_bn(P, pe + ".2", h, 1, 1, trk=trk, updates=1)
     if acts is not None:
@@ -154,9 +177,10 @@ def forward_stage3(P, x, trk=None, prefix="encoder.", acts=None, depths=DEPTHS):
             j0 = 1
         for j in range(depths[i]):
             if i == 0:
-                h = _mbconv(P, sp + str(j0 + j), h, EMBED[0], EMBED[0], 1, trk, 2)
+                h = _mbconv(P, sp + str(j0 + j), h, EMBED[0], EMBED[0], 1, trk, 2, dpr[cur])
             else:
-                h = _vit_block(P, sp + str(j0 + j), h, HEADS[i])
+                h = _vit_block(P, sp + str(j0 + j), h, HEADS[i], dpr[cur])
+            cur += 1
         if acts is not None:
             acts[f"act_stage{i}"] = h
     return h
@@ -169,16 +193,21 @@ def _decoder_layer(P, pre, x, heads):
     h = _ln(P, pre + ".norm1", x)
     qkv = h @ P[pre + ".self_attn.in_proj_weight"].t() + P[pre + ".self_attn.in_proj_bias"]
     q, k, v = (t.reshape(B, L, heads, d).transpose(1, 2) for t in qkv.split(D, dim=-1))
-    a = _attention_core(q, k, v).transpose(1, 2).reshape(B, L, D)
-    x = x + (a @ P[pre + ".self_attn.out_proj.weight"].t() + P[pre + ".self_attn.out_proj.bias"])
+    if _DROP["on"]:   # nn.MultiheadAttention(dropout=0.1) on the probabilities (explicit, as MHA's math path)
+        pr = F.dropout(torch.softmax((q @ k.transpose(-2, -1)) / math.sqrt(d), -1), 0.1, training=True)
+        a = (pr @ v).transpose(1, 2).reshape(B, L, D)
+    else:
+        a = _attention_core(q, k, v).transpose(1, 2).reshape(B, L, D)
+    x = x + _dropout(a @ P[pre + ".self_attn.out_proj.weight"].t() + P[pre + ".self_attn.out_proj.bias"])
     h = _ln(P, pre + ".norm2", x)
-    h = F.gelu(h @ P[pre + ".linear1.weight"].t() + P[pre + ".linear1.bias"])
-    return x + (h @ P[pre + ".linear2.weight"].t() + P[pre + ".linear2.bias"])
+    h = _dropout(F.gelu(h @ P[pre + ".linear1.weight"].t() + P[pre + ".linear1.bias"]))
+    return x + _dropout(h @ P[pre + ".linear2.weight"].t() + P[pre + ".linear2.bias"])
 
 
 def mae_forward(P, clip, mask, cfg, trk=None, acts=None):
     """TinyVideoMAE.forward (mae_vit_adapter.py:75-117) -> pred [B, T*L, 192]."""
     B, C, T, H, W = clip.shape
+    _DROP["on"] = bool(cfg.get("train_dropout", False))
     frames = clip.permute(0, 2, 1, 3, 4).reshape(B * T, C, H, W)
     lat = forward_stage3(P, frames, trk, acts=acts, depths=depths_of(cfg))
     Lp = lat.shape[2] * lat.shape[3]
