@@ -94,8 +94,8 @@ def test_bf16_stage_outputs_vs_oracle_c2_clip(golden_dir):
     ours = {}
     pe_run, st_run = TV.PatchEmbed.run, TV._Stage.run
 
-    def pe(self, x, mode):
-        t, xbn = pe_run(self, x, mode)
+    def pe(self, x, mode, fold_ok=True):
+        t, xbn = pe_run(self, x, mode, fold_ok)
         if "act_stem" not in ours:   # the stem output y = BN2(a2) (formed here when BN2 is folded)
             y = t if xbn is None else K.bn_apply(t.reshape(-1, t.shape[-1]), *xbn[:4], gelu=False).view(t.shape)
             ours["act_stem"] = y.detach().float().permute(0, 3, 1, 2).cpu()
