@@ -289,6 +289,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     peak_mem = torch.cuda.max_memory_allocated(dev) / 2 ** 30
+    if os.environ.get("SM_BENCH_MEMSTATS"):   # allocator behaviour over the whole run (A/B diagnostics)
+        ms_ = torch.cuda.memory_stats(dev)
+        print("[bench] allocator: " + " ".join(f"{k}={ms_.get(k)}" for k in (
+            "num_alloc_retries", "num_device_alloc", "num_device_free", "num_sync_all_streams",
+            "reserved_bytes.all.peak", "allocated_bytes.all.peak")), file=sys.stderr)
 
     if rank == 0:
         clips_total = B * world * args.steps

@@ -72,6 +72,21 @@ def gemm(args):
         torch.cuda.empty_cache()
 
 
+def bnstats(args):
+    """Linear + output BatchNorm statistics (linear_bn_stats: the MBConv expand convs) against
+    the plain linear of the same shape: the statistics epilogue's cost."""
+    B = args.batch
+    for name, M, N, Kd in [("s0 expand+stats", B * 8 * 12544, 384, 96), ("s1 expand+stats", B * 8 * 3136, 768, 192)]:
+        x = torch.randn(M, Kd, device="cuda").to(torch.bfloat16)
+        w = torch.randn(N, Kd, device="cuda").to(torch.bfloat16)
+        t0 = timeit(lambda: K.linear(x, w), args.iters)
+        t1 = timeit(lambda: K.linear_bn_stats(x, w), args.iters)
+        print(f"{name}: M={M} N={N} K={Kd}  linear {t0:7.3f} ms | linear_bn_stats {t1:7.3f} ms "
+              f"(statistics +{t1 - t0:6.3f} ms)", flush=True)
+        del x, w
+        torch.cuda.empty_cache()
+
+
 def dw(args):
     """Every weight-gradient GEMM shape of the step: dW[nout][nin] = dy^T x (+ db)."""
     B = args.batch
@@ -280,7 +295,8 @@ def mbconv(args):
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["attn", "gemm", "gemmk", "mbconv", "dw", "dwx", "dwse", "stem", "gemmw"])
+    ap.add_argument("what", choices=["attn", "gemm", "gemmk", "mbconv", "dw", "dwx", "dwse", "stem", "gemmw",
+                                     "bnstats"])
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--drop", type=float, default=0.1)
     ap.add_argument("--iters", type=int, default=5)
@@ -288,4 +304,5 @@ if __name__ == "__main__":
     a = ap.parse_args()
     from ssl_mae_amd.build import build
     build()
-    {"attn": attn, "gemm": gemm, "gemmk": gemmk, "mbconv": mbconv, "dw": dw, "dwx": dwx, "dwse": dwse, "stem": stem, "gemmw": gemmw}[a.what](a)
+    {"attn": attn, "gemm": gemm, "gemmk": gemmk, "mbconv": mbconv, "dw": dw, "dwx": dwx, "dwse": dwse, "stem": stem, "gemmw": gemmw,
+     "bnstats": bnstats}[a.what](a)

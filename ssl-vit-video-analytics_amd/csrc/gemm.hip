@@ -165,6 +165,40 @@ SM_DEV bf16x8 lread_frag(const char* lds, int rb, int s) {
 // banks: a 2-way conflict on every run write, 44 % extra LDS cycles in the stage-0
 // expand GEMM, profiles/r04g_gemm_sq_counters.txt.)
 SM_DEV int rs_swz(int row) { return (row ^ (row >> 3)) & 7; }
+// v + v(lane ^ 8) + v(lane ^ 16) + v(lane ^ 32), summed in that order (= three __shfl_xor
+// steps, bit for bit: each step adds one partner, and the two operands of an add commute):
+// a DPP row rotate by 8 and two lane swaps instead of three ds_bpermute round trips
+SM_DEV float xor8_16_32_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xF, 0xF, false));   // row_ror:8
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+// per-lane column sums / sums of squares of one 16-B run of 8 bf16 outputs (masked by `in`),
+// as packed pairs (v_pk_add_f32 / v_pk_fma_f32: the per-element add and fma, two per issue)
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+SM_DEV void stats_acc8(uint4 v, bool in, float* st1, float* st2) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t u = in ? w[q] : 0u;
+    const f32x2_t f = {__uint_as_float(u << 16), __uint_as_float(u & 0xFFFF0000u)};
+    f32x2_t a = {st1[2 * q], st1[2 * q + 1]}, b = {st2[2 * q], st2[2 * q + 1]};
+    a = a + f;
+    b = __builtin_elementwise_fma(f, f, b);
+    st1[2 * q] = a.x; st1[2 * q + 1] = a.y;
+    st2[2 * q] = b.x; st2[2 * q + 1] = b.y;
+  }
+}
+// the wave's per-lane partials -> totals of its 8 lane groups (lanes l & 7 = one 8-column chunk)
+SM_DEV void stats_reduce8(float* st1, float* st2) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    st1[e] = xor8_16_32_sum(st1[e]);
+    st2[e] = xor8_16_32_sum(st2[e]);
+  }
+}
 struct RowStage {
   char* base;   // this wave's 2 x 4 KB: [0] C, [1] aux
   SM_DEV void put(int region, int row, int chunk, uint4 v) const {
@@ -172,50 +206,24 @@ struct RowStage {
   }
   // rows: tile rows [row0, row0 + 32) of out (ld elements) at column col0; 16-B chunk
   // c holds `cpc` columns; rows >= M or chunk columns >= N are not stored
-  // st1 / st2 (bf16 images): column sums / sums of squares of the stored rows of this
-  // 32-row image accumulated into lanes 0..7 (chunk l = 8 columns), for BatchNorm
-  // statistics of the output
+  // st1 / st2 (bf16 images): this lane's partial column sums / sums of squares of the
+  // stored rows of this 32-row image (its chunk l & 7 = 8 columns), for BatchNorm
+  // statistics of the output; stats_reduce8 totals them over the lane groups once per tile
   template <typename TC, bool STATS = false>
   SM_DEV void flush(int region, TC* out, int64_t ld, int64_t row0, int col0, int M, int N, int l,
                     float* st1 = nullptr, float* st2 = nullptr, int wcols = 128 / (int)sizeof(TC)) const {
     constexpr int cpc = 16 / sizeof(TC);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const int c = l & 7;
-    float a1[8], a2[8];
-    if constexpr (STATS) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) a1[e] = a2[e] = 0.f;
-    }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int r = (l >> 3) + 8 * q;
       const uint4 v = *(const uint4*)(base + region * 4096 + r * 128 + ((c ^ rs_swz(r)) << 4));
       const int64_t row = row0 + r;
       const int col = col0 + c * cpc;
-      if (row < M && col < N && c * cpc < wcols) {   // wcols: the wave's own columns of the image
-        *(uint4*)(out + row * ld + col) = v;
-        if constexpr (STATS) {
-          const bf16x8 b = __builtin_bit_cast(bf16x8, v);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float f = (float)b[e];
-            a1[e] += f;
-            a2[e] = fmaf(f, f, a2[e]);
-          }
-        }
-      }
-    }
-    if constexpr (STATS) {   // the 8 row groups (l >> 3) of each chunk, fixed order
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-#pragma unroll
-        for (int x = 8; x < 64; x <<= 1) {
-          a1[e] += __shfl_xor(a1[e], x, 64);
-          a2[e] += __shfl_xor(a2[e], x, 64);
-        }
-        st1[e] += a1[e];
-        st2[e] += a2[e];
-      }
+      const bool ok = row < M && col < N && c * cpc < wcols;   // wcols: the wave's own columns of the image
+      if (ok) *(uint4*)(out + row * ld + col) = v;
+      if constexpr (STATS) stats_acc8(v, ok, st1, st2);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
@@ -451,6 +459,9 @@ SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x
       if constexpr (STATS) rs_.flush<TC, true>(0, (TC*)g.C, g.ldc, r0, c0, g.M, g.N, l, st1, st2);
       else rs_.flush<TC>(0, (TC*)g.C, g.ldc, r0, c0, g.M, g.N, l, nullptr, nullptr, 32 * NJ);
     }
+  }
+  if constexpr (STATS) {
+    if (stage && sizeof(TC) == 2) stats_reduce8(st1, st2);   // every lane (lane swaps)
   }
   if (STATS && stage && sizeof(TC) == 2 && l < 8 && m0 + wm < g.M) {   // this wave's 64 rows x 64 cols
     const int wrow = (m0 + wm) >> 6;                         // part row = 64-row slab of the output
@@ -1152,41 +1163,16 @@ SM_DEV __attribute__((always_inline)) void pp_flush(const GemmArgs& g, int m0, i
     const int r0 = m0 + wm + 32 * i;
     const int rows_valid = g.M - r0;
     const auto rs = rows_rsrc((const __bf16*)g.C + (int64_t)r0 * g.ldc, rows_valid, g.ldc * 2);
-    float a1[8], a2[8];
-    if constexpr (STATS) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) a1[e] = a2[e] = 0.f;
-    }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int r = (l >> 3) + 8 * q;
       const uint4 v = *(const uint4*)(img + i * 4096 + r * 128 + ((c ^ rs_swz(r)) << 4));
       bstore128(v, rs, cok ? (uint32_t)((r * g.ldc + col) * 2) : BUF_OOB);
-      if constexpr (STATS) {
-        const bool in = cok && r < rows_valid;
-        const bf16x8 b = __builtin_bit_cast(bf16x8, v);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float f = in ? (float)b[e] : 0.f;
-          a1[e] += f;
-          a2[e] = fmaf(f, f, a2[e]);
-        }
-      }
-    }
-    if constexpr (STATS) {   // the 8 row groups (l >> 3) of each chunk, fixed order (RowStage::flush)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-#pragma unroll
-        for (int x = 8; x < 64; x <<= 1) {
-          a1[e] += __shfl_xor(a1[e], x, 64);
-          a2[e] += __shfl_xor(a2[e], x, 64);
-        }
-        st1[e] += a1[e];
-        st2[e] += a2[e];
-      }
+      if constexpr (STATS) stats_acc8(v, cok && r < rows_valid, st1, st2);   // (RowStage::flush's order)
     }
   }
   if constexpr (STATS) {   // this wave's 64 rows x 64 columns -> part row (m0 + wm) / 64, lanes 0..7
+    stats_reduce8(st1, st2);
     const int wrow = (m0 + wm) >> 6;
     const int sc = n0 + wn + 8 * l;
     const auto prs = __builtin_amdgcn_make_buffer_rsrc((void*)(g.stat_part + (int64_t)wrow * 2 * g.N), (short)0,
