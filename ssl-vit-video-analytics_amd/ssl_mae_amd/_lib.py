@@ -9,7 +9,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsslmae.so")
+# SM_LIB_PATH: another build of the same library (same-box A/B of two builds, scripts/ab_lib.sh)
+LIB_PATH = os.environ.get("SM_LIB_PATH") or os.path.join(_HERE, "libsslmae.so")
 
 F32, BF16 = 0, 1
 _DT = {torch.float32: F32, torch.bfloat16: BF16}
