@@ -1423,14 +1423,15 @@ __global__ __launch_bounds__(256) void dwb_dx_kernel(const __bf16* x, ChanAffine
   // so the compiler cannot hoist the next row's loads above this row's store by itself
   // (one 32-B load pair in flight per lane streamed at ~4.4 TB/s)
   constexpr int U = 4;
+  typedef unsigned int nt4 __attribute__((ext_vector_type(4)));
   int64_t row = r0 + r;
   for (; row + (U - 1) * rpp < r1; row += U * rpp) {
-    uint4 xr[U], dr[U];
+    nt4 xr[U], dr[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
+    for (int u = 0; u < U; ++u) {   // streamed once: non-temporal loads and stores
       const int64_t e = (row + u * rpp) * C + chunk * 8;
-      xr[u] = *(const uint4*)(x + e);
-      dr[u] = *(const uint4*)(dz + e);
+      xr[u] = __builtin_nontemporal_load((const nt4*)(x + e));
+      dr[u] = __builtin_nontemporal_load((const nt4*)(dz + e));
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -1439,7 +1440,10 @@ __global__ __launch_bounds__(256) void dwb_dx_kernel(const __bf16* x, ChanAffine
       load8((const __bf16*)&dr[u], dv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = wr[j] * (dv[j] - k0[j] - (xv[j] - mu[j]) * rs[j] * k1[j]);
-      store8(dz + (row + u * rpp) * C + chunk * 8, o);
+      bf16x8 ob;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ob[j] = (__bf16)o[j];
+      __builtin_nontemporal_store(__builtin_bit_cast(nt4, ob), (nt4*)(dz + (row + u * rpp) * C + chunk * 8));
     }
   }
   for (; row < r1; row += rpp) {
