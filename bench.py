@@ -50,6 +50,10 @@ def parse():
     ap.add_argument("--lite", default="",
                     help="encoder stages kept lite-resident (MBConv a1/a2 recomputed in the backward instead of "
                          "the whole stage): comma list or 'none'; default: the model's auto policy")
+    ap.add_argument("--arena", default="auto", choices=["auto", "on", "off"],
+                    help="device-memory arena (ssl_mae_amd/arena.py) instead of the caching allocator: "
+                         "auto = on for the MAE step (its stage-0 resident policy needs the arena's "
+                         "coalescing heap), off for the fine-tune step")
     ap.add_argument("--probe", default="dec_attn_bwd",
                     help="kernel group timed with events for the roofline line: dec_attn_bwd (the top-time "
                          "kernels of the step: decoder attention dK/dV + dQ) or dec_attn_fwd")
@@ -192,6 +196,9 @@ def lite_used(model, frames, S):
 
 def main():
     args = parse()
+    if args.arena == "on" or (args.arena == "auto" and args.workload == "mae"):
+        from ssl_mae_amd import arena as smarena
+        smarena.install()               # before the first CUDA allocation of the process
     from ssl_mae_amd import dist as smdist
     from ssl_mae_amd import kernels as K
     from ssl_mae_amd.build import build
@@ -288,8 +295,17 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-    peak_mem = torch.cuda.max_memory_allocated(dev) / 2 ** 30
-    if os.environ.get("SM_BENCH_MEMSTATS"):   # allocator behaviour over the whole run (A/B diagnostics)
+    from ssl_mae_amd import arena as smarena
+    peak_mem = smarena.max_memory_allocated(dev) / 2 ** 30
+    if smarena.active() and os.environ.get("SM_BENCH_MEMSTATS"):
+        print("[bench] arena: " + " ".join(f"{k}={v}" for k, v in smarena.stats(dev).items()), file=sys.stderr)
+    if os.environ.get("SM_BENCH_SNAPSHOT") and not smarena.active():   # caching-allocator segments (diagnostics)
+        segs = torch.cuda.memory_snapshot()
+        summary = [{"size": sg["total_size"], "allocated": sg["allocated_size"], "stream": sg.get("stream"),
+                    "blocks": [(b["size"], b["state"]) for b in sg["blocks"]][:64]} for sg in segs]
+        with open(os.environ["SM_BENCH_SNAPSHOT"], "w") as fh:
+            json.dump(summary, fh)
+    if os.environ.get("SM_BENCH_MEMSTATS") and not smarena.active():   # allocator behaviour (A/B diagnostics)
         ms_ = torch.cuda.memory_stats(dev)
         print("[bench] allocator: " + " ".join(f"{k}={ms_.get(k)}" for k in (
             "num_alloc_retries", "num_device_alloc", "num_device_free", "num_sync_all_streams",
@@ -350,6 +366,9 @@ def main():
             "model_tflops_per_gpu": round(step_tflops, 1) if step_tflops else None,
             "model_mfu": round(step_tflops / MFMA_BF16_PEAK_TFLOPS, 4) if step_tflops else None,
             "peak_mem_gib": round(peak_mem, 1),
+            "allocator": ({"kind": "arena", "capacity_gib": round(smarena.stats(dev)["capacity"] / 2 ** 30, 1),
+                           "hipmalloc_requests": smarena.stats(dev)["hipmalloc_requests"]}
+                          if smarena.active() else {"kind": "caching"}),
             "loss_first_last": [round(loss_vals[0], 5), round(loss_vals[-1], 5)],
             "loss_item_per_step": True,
             "cpu_baseline": cpu,

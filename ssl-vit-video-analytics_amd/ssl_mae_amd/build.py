@@ -97,5 +97,27 @@ def build(verbose=False, jobs=None):
     return LIB
 
 
+ARENA_SRC = os.path.join(CSRC, "arena.cpp")
+ARENA_LIB = os.path.join(PKG_DIR, "libsmarena.so")
+
+
+def build_arena():
+    """Host-only C++ (csrc/arena.cpp, the device-memory arena behind PyTorch's
+    pluggable-allocator hook) into libsmarena.so, linked against the HIP runtime."""
+    if os.path.exists(ARENA_LIB) and os.path.getmtime(ARENA_LIB) >= os.path.getmtime(ARENA_SRC):
+        return ARENA_LIB
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    tmp = ARENA_LIB + ".tmp"
+    cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall",
+           "-D__HIP_PLATFORM_AMD__", "-I", os.path.join(rocm, "include"), ARENA_SRC,
+           "-L", os.path.join(rocm, "lib"), "-lamdhip64", f"-Wl,-rpath,{os.path.join(rocm, 'lib')}", "-o", tmp]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"arena build failed:\n{r.stderr[-4000:]}")
+    os.replace(tmp, ARENA_LIB)
+    return ARENA_LIB
+
+
 if __name__ == "__main__":
     print(build(verbose=True))
+    print(build_arena())

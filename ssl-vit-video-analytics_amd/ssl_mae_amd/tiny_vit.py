@@ -302,22 +302,35 @@ class TinyViT(nn.Module):
 # (encoder depths, decoder depth); activations scale with the pixel count, fp32
 # doubles them.  An unlisted model takes the reference's policy (all checkpointed).
 _PEAK_GIB_PER_FRAME = {
-    ((2, 2, 6, 2), 4): {(1, 2): 216.0 / 2048, (2,): 171.9 / 2048, (): 143.6 / 2048},
+    # (0, 1, 2): stage 0 resident too, 2 x 131.9 GiB at B = 128 less the B-independent 0.7 GiB
+    ((2, 2, 6, 2), 4): {(0, 1, 2): 263.1 / 2048, (1, 2): 216.0 / 2048, (2,): 171.9 / 2048, (): 143.6 / 2048},
     # C3 ViT-Small (depths 2,2,12,2 + 8-layer decoder): (2,) and (1, 2) exceed 288 GB at B=256
     ((2, 2, 12, 2), 8): {(): 184.0 / 2048},
 }
 
 
-def auto_resident_stages(frames, image_size, bf16, device, budget=0.85, key=((2, 2, 6, 2), 4)):
+def auto_resident_stages(frames, image_size, bf16, device, budget=0.85, key=((2, 2, 6, 2), 4),
+                         arena_budget=0.96):
     """The largest resident set whose predicted step peak fits `budget` of the
-    device memory (stage 0, the 112x112 MBConvs, is always recomputed)."""
+    device memory.  Stage 0 (the 112x112 MBConvs) is resident only under the
+    device-memory arena (ssl_mae_amd/arena.py) and when the prediction fits
+    `arena_budget` of its capacity: the caching allocator's exact-size segments
+    leave ~50 GB of slack at B = 256, which the 263 GiB of that policy do not
+    survive (profiles/r05ik_allocator_policy.txt)."""
     table = _PEAK_GIB_PER_FRAME.get(key)
     if table is None:
         return ()
     total = torch.cuda.get_device_properties(device).total_memory / 2 ** 30
     scale = frames * (image_size / 224.0) ** 2 * (1 if bf16 else 2)
-    for policy in ((1, 2), (2,)):
-        if policy in table and table[policy] * scale <= budget * total:
+    for policy in ((0, 1, 2), (1, 2), (2,)):
+        if policy not in table:
+            continue
+        if 0 in policy:
+            from . import arena
+            cap = arena.capacity_gib(device) if arena.active() else 0.0
+            if cap and table[policy] * scale <= arena_budget * cap:
+                return policy
+        elif table[policy] * scale <= budget * total:
             return policy
     return ()
 

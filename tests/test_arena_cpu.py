@@ -1,0 +1,106 @@
+"""Device-memory arena (csrc/arena.cpp): placement and coalescing, checked over a
+host buffer attached to an unused device slot (sm_arena_attach; no HIP call is
+made and arena memory is never dereferenced)."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "ssl-vit-video-analytics_amd"))
+
+from ssl_mae_amd import arena  # noqa: E402
+
+MIB = 1 << 20
+
+
+def _attach(slot, cap):
+    lib = arena.library()
+    base = 1 << 40                              # a fake range: the arena never dereferences its memory
+    assert lib.sm_arena_attach(slot, ctypes.c_void_p(base), cap) == 0
+    assert lib.sm_arena_attach(slot, ctypes.c_void_p(base), cap) == -1   # slot taken
+    return lib, base
+
+
+def test_exports():
+    lib = arena.library()
+    for sym in ("sm_arena_alloc", "sm_arena_free", "sm_arena_stats", "sm_arena_reset_peak", "sm_arena_attach"):
+        assert hasattr(lib, sym)
+
+
+def test_best_fit_and_coalescing():
+    slot = 13
+    lib, base = _attach(slot, 64 * MIB)
+    a = lib.sm_arena_alloc(1 * MIB, slot, None)
+    b = lib.sm_arena_alloc(4 * MIB, slot, None)
+    c = lib.sm_arena_alloc(1 * MIB, slot, None)
+    d = lib.sm_arena_alloc(2 * MIB, slot, None)
+    assert [a, b, c, d] == [base, base + MIB, base + 5 * MIB, base + 6 * MIB]
+    lib.sm_arena_free(b, 4 * MIB, slot, None)
+    # best fit: the 4 MiB hole beats the 56 MiB tail, lowest address first
+    e = lib.sm_arena_alloc(3 * MIB, slot, None)
+    assert e == b
+    f = lib.sm_arena_alloc(1 * MIB, slot, None)
+    assert f == b + 3 * MIB
+    s = arena.stats(slot)
+    assert s["in_use"] == 8 * MIB and s["peak"] == 8 * MIB and s["free_blocks"] == 1
+    for p, n in ((a, MIB), (c, MIB), (e, 3 * MIB), (d, 2 * MIB), (f, MIB)):
+        lib.sm_arena_free(p, n, slot, None)
+    s = arena.stats(slot)
+    assert s["in_use"] == 0 and s["free_blocks"] == 1 and s["largest_free"] == 64 * MIB
+    lib.sm_arena_reset_peak(slot)
+    assert arena.stats(slot)["peak"] == 0
+
+
+def test_random_sequence_no_overlap_full_coalesce():
+    slot = 14
+    cap = 256 * MIB
+    lib, base = _attach(slot, cap)
+    rng = np.random.default_rng(5)
+    live = {}
+    for step in range(4000):
+        if live and (rng.random() < 0.45 or len(live) > 60):
+            p = list(live)[rng.integers(len(live))]
+            lib.sm_arena_free(p, live.pop(p), slot, None)
+            continue
+        n = int(rng.choice([1, 700, 4096, 100_000, MIB, 3 * MIB + 17, 9 * MIB]))
+        p = lib.sm_arena_alloc(n, slot, None)
+        if p is None:                 # full: the hipMalloc fallback fails without a GPU
+            continue
+        assert p % 512 == 0 and base <= p and p + n <= base + cap
+        live[p] = n
+        if step % 97 == 0:
+            spans = sorted((q, q + ((m + 511) // 512) * 512) for q, m in live.items())
+            assert all(e0 <= s1 for (_, e0), (s1, _) in zip(spans, spans[1:])), "overlapping blocks"
+            assert arena.stats(slot)["in_use"] == sum(e - s for s, e in spans)
+    for p, n in live.items():
+        lib.sm_arena_free(p, n, slot, None)
+    s = arena.stats(slot)
+    assert s["in_use"] == 0 and s["free_blocks"] == 1 and s["largest_free"] == cap
+
+
+def test_zero_size_request_gets_a_block():
+    slot = 15
+    lib, base = _attach(slot, 4 * MIB)
+    p = lib.sm_arena_alloc(0, slot, None)
+    assert p == base
+    lib.sm_arena_free(p, 0, slot, None)
+    assert arena.stats(slot)["in_use"] == 0
+
+
+@pytest.mark.parametrize("policy_cap, expect", [(0.0, (1, 2)), (200.0, (1, 2)), (281.0, (0, 1, 2))])
+def test_stage0_resident_policy_needs_arena(monkeypatch, policy_cap, expect):
+    """auto_resident_stages: stage 0 resident only under an arena whose capacity
+    holds the predicted 263 GiB at B = 256 (T = 8, 224^2, bf16)."""
+    import torch
+    from ssl_mae_amd import tiny_vit as TV
+
+    class Props:
+        total_memory = 288 * 2 ** 30
+    monkeypatch.setattr(torch.cuda, "get_device_properties", lambda d: Props())
+    monkeypatch.setattr(arena, "active", lambda: policy_cap > 0)
+    monkeypatch.setattr(arena, "capacity_gib", lambda d=None: policy_cap)
+    assert TV.auto_resident_stages(256 * 8, 224, True, "cuda") == expect
+    assert TV.auto_lite_stages(256 * 8, 224, True, "cuda", expect) == ((0,) if expect == (1, 2) else ())
