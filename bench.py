@@ -198,7 +198,9 @@ def main():
     args = parse()
     if args.arena == "on" or (args.arena == "auto" and args.workload == "mae"):
         from ssl_mae_amd import arena as smarena
-        smarena.install()               # before the first CUDA allocation of the process
+        # before the first CUDA allocation of the process; ranks of a multi-GPU run
+        # leave RCCL's channel buffers 8 GiB outside the heap
+        smarena.install(reserve_mib=8192 if int(os.environ.get("WORLD_SIZE", "1")) > 1 else None)
     from ssl_mae_amd import dist as smdist
     from ssl_mae_amd import kernels as K
     from ssl_mae_amd.build import build
