@@ -169,8 +169,15 @@ def main(argv=None):
     ap.add_argument("--config", default="configs/ssl_mae.yaml")
     ap.add_argument("--resume", default=None, help="training-state file written by a previous run")
     ap.add_argument("--max-steps", type=int, default=None, help="stop each epoch after this many steps")
+    ap.add_argument("--arena", action="store_true",
+                    help="device-memory arena instead of the caching allocator (ssl_mae_amd/arena.py; "
+                         "lets the memory policy keep stage 0 resident at large batches); must be the "
+                         "process's first CUDA use")
     args = ap.parse_args(argv)
     cfg = load_config(args.config)
+    if args.arena:
+        from . import arena
+        arena.install(reserve_mib=8192 if int(os.environ.get("WORLD_SIZE", "1")) > 1 else None)
     rank, world = smdist.init_from_env()          # torchrun: one process per GPU (RCCL)
     set_seed(42)
     local = int(os.environ.get("LOCAL_RANK", "0")) if world > 1 else torch.cuda.current_device()
