@@ -59,6 +59,45 @@ SM_DEV void store4(__bf16* p, const float* v) {
   for (int i = 0; i < 4; ++i) a[i] = (__bf16)v[i];
   *(bf16x4*)p = a;
 }
+// The same with the non-temporal hint (`nt` loads / stores): for tensors a kernel streams
+// once, larger than the caches, so they do not evict lines other waves still reuse.
+SM_DEV void load8_nt(const float* p, float* v) {
+  const f32x4 a = __builtin_nontemporal_load((const f32x4*)p), b = __builtin_nontemporal_load((const f32x4*)p + 1);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { v[i] = a[i]; v[4 + i] = b[i]; }
+}
+SM_DEV void load8_nt(const __bf16* p, float* v) {
+  const bf16x8 a = __builtin_nontemporal_load((const bf16x8*)p);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = (float)a[i];
+}
+SM_DEV void store8_nt(float* p, const float* v) {
+  __builtin_nontemporal_store(f32x4{v[0], v[1], v[2], v[3]}, (f32x4*)p);
+  __builtin_nontemporal_store(f32x4{v[4], v[5], v[6], v[7]}, (f32x4*)p + 1);
+}
+SM_DEV void store8_nt(__bf16* p, const float* v) {
+  bf16x8 a;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = (__bf16)v[i];
+  __builtin_nontemporal_store(a, (bf16x8*)p);
+}
+SM_DEV void load4_nt(const float* p, float* v) {
+  const f32x4 a = __builtin_nontemporal_load((const f32x4*)p);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = a[i];
+}
+SM_DEV void load4_nt(const __bf16* p, float* v) {
+  const bf16x4 a = __builtin_nontemporal_load((const bf16x4*)p);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = (float)a[i];
+}
+SM_DEV void store4_nt(float* p, const float* v) { __builtin_nontemporal_store(f32x4{v[0], v[1], v[2], v[3]}, (f32x4*)p); }
+SM_DEV void store4_nt(__bf16* p, const float* v) {
+  bf16x4 a;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) a[i] = (__bf16)v[i];
+  __builtin_nontemporal_store(a, (bf16x4*)p);
+}
 
 // ---------------------------------------------------------------- math
 // Exact (erf) GELU, nn.GELU's default.  Phi(x) = 0.5 (1 + erf(x / sqrt 2)) is formed

@@ -1556,11 +1556,11 @@ __global__ __launch_bounds__(256) void se_reduce_kernel(const T* x, const T* dy,
     for (int p = p0 + cm.r; p < p1; p += cm.rpp) {
       const int64_t e = (f * HW + p) * C + cm.c0;
       float v[8];
-      load8(x + e, v);
+      load8_nt(x + e, v);
       af.apply<T>(v);
       if (dy) {
         float g[8];
-        load8(dy + e, g);
+        load8_nt(dy + e, g);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] *= g[j];
       }
@@ -1721,8 +1721,8 @@ __global__ __launch_bounds__(256) void se_bn_reduce_kernel(const T* dy, const T*
     for (int p = p0 + cm.r; p < p1; p += cm.rpp) {
       const int64_t e = (f * HW + p) * C + cm.c0;
       float v[8], g[8];
-      load8(x + e, v);
-      load8(dy + e, g);
+      load8_nt(x + e, v);
+      load8_nt(dy + e, g);
 #pragma unroll
       for (int j = 0; j < 8; j += 2) {   // packed pairs (gelu_phi_pair_t)
         const f32x2 vv = f32x2{v[j], v[j + 1]};
@@ -1824,8 +1824,8 @@ __global__ __launch_bounds__(256) void se_bn_dx_kernel(const T* dy, const T* x, 
   for (int p = p0 + cm.r; p < p1; p += cm.rpp) {
     const int64_t e = (f * HW + p) * C + cm.c0;
     float v[8], g[8], o[8];
-    load8(x + e, v);
-    load8(dy + e, g);
+    load8_nt(x + e, v);
+    load8_nt(dy + e, g);
 #pragma unroll
     for (int j = 0; j < 8; j += 2) {   // packed pairs (gelu_phi_pair_t)
       f32x2 gd = f32x2{1.f, 1.f};
@@ -1835,7 +1835,7 @@ __global__ __launch_bounds__(256) void se_bn_dx_kernel(const T* dy, const T* x, 
       for (int i = 0; i < 2; ++i)
         o[j + i] = fmaf(gd[i], fmaf(g[j + i], ka[j + i], kb[j + i]), fmaf(-c1[j + i], v[j + i], c0[j + i]));
     }
-    store8(dx + e, o);
+    store8_nt(dx + e, o);
   }
 }
 

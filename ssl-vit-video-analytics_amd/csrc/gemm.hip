@@ -222,7 +222,10 @@ struct RowStage {
       const int64_t row = row0 + r;
       const int col = col0 + c * cpc;
       const bool ok = row < M && col < N && c * cpc < wcols;   // wcols: the wave's own columns of the image
-      if (ok) *(uint4*)(out + row * ld + col) = v;
+      // non-temporal: the output streams past L2, where the operand panels the tile's
+      // neighbours still read live
+      typedef __attribute__((ext_vector_type(4))) unsigned int u32x4s;
+      if (ok) __builtin_nontemporal_store(u32x4s{v.x, v.y, v.z, v.w}, (u32x4s*)(out + row * ld + col));
       if constexpr (STATS) stats_acc8(v, ok, st1, st2);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1051,7 +1054,7 @@ SM_DEV int opaque_tid() {
 
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 SM_DEV void bstore128(uint4 v, __amdgpu_buffer_rsrc_t rs, uint32_t off) {
-  __builtin_amdgcn_raw_buffer_store_b128(u32x4{v.x, v.y, v.z, v.w}, rs, off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(u32x4{v.x, v.y, v.z, v.w}, rs, off, 0, 2);   // aux 2: nt
 }
 
 // descriptor over rows [0, rows_valid) of a row-major matrix (row_bytes apart) at base

@@ -177,7 +177,7 @@ __global__ __launch_bounds__(256) void ln_fwd16_kernel(const TI* x, const float*
     float s = 0.f;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      load4(xr + 64 * u, v[u]);
+      load4_nt(xr + 64 * u, v[u]);
       s += (v[u][0] + v[u][1]) + (v[u][2] + v[u][3]);
     }
     const float mu = sum16(s) * (1.f / C);
@@ -193,7 +193,7 @@ __global__ __launch_bounds__(256) void ln_fwd16_kernel(const TI* x, const float*
       float o[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[j] = (v[u][j] - mu) * rs * gg[u][j] + bb[u][j];
-      store4(yr + 64 * u, o);
+      store4(yr + 64 * u, o);   // (read back by the next GEMM: a normal store measured faster for bf16 x)
     }
     if (gl == 0) { mean[row] = mu; rstd[row] = rs; }
   }
@@ -253,8 +253,8 @@ __global__ __launch_bounds__(256) void ln_bwd16_kernel(const TD* dy, const TI* x
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       float xv[4], dv[4];
-      load4(x + e0 + 4 * G * u, xv);
-      load4(dy + e0 + 4 * G * u, dv);
+      load4_nt(x + e0 + 4 * G * u, xv);
+      load4_nt(dy + e0 + 4 * G * u, dv);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         xh[u][j] = (xv[j] - mu) * rs;
@@ -274,11 +274,11 @@ __global__ __launch_bounds__(256) void ln_bwd16_kernel(const TD* dy, const TI* x
       for (int j = 0; j < 4; ++j) o[j] = rs * (gy[u][j] - s1 - xh[u][j] * s2);
       if (dres) {
         float pr[4];
-        load4(dres + e0 + 4 * G * u, pr);
+        load4_nt(dres + e0 + 4 * G * u, pr);
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[j] += pr[j];
       }
-      store4(dx + e0 + 4 * G * u, o);
+      store4_nt(dx + e0 + 4 * G * u, o);
       if (br.bo) {
         const float rsv = br.rs ? br.rs[row / br.rpg] : 1.f;
         const float ks = br.p > 0.f ? 1.f / (1.f - br.p) : 1.f;
@@ -292,7 +292,7 @@ __global__ __launch_bounds__(256) void ln_bwd16_kernel(const TD* dy, const TI* x
           const float mj = br.p > 0.f ? (((hsh >> (8 * j)) & 0xFFu) >= thr ? ks : 0.f) : 1.f;
           b4[j] = d * (rsv * mj);
         }
-        store4(br.bo + e0 + 4 * G * u, b4);
+        store4_nt(br.bo + e0 + 4 * G * u, b4);
       }
     }
   }
@@ -441,7 +441,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const TI* x, const float*
   for (int64_t row = r0 + cm.r; row < r1; row += cm.rpp) {
     const int64_t e = row * C + cm.chunk * 8;
     float v[8];
-    load8(x + e, v);
+    load8_nt(x + e, v);
 #pragma unroll
     for (int j = 0; j < 8; j += 2) {   // packed pairs (gelu_phi_pair_t); = Affine8::apply
       f32x2 t = vfma(f32x2{v[j], v[j + 1]}, f32x2{sc[j], sc[j + 1]}, f32x2{sh[j], sh[j + 1]});
@@ -456,12 +456,12 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const TI* x, const float*
     }
     if (R) {
       float rr[8];
-      load8(R + e, rr);
+      load8_nt(R + e, rr);
       ra.apply<TO>(rr);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] += rr[j];
     }
-    store8(y + e, v);
+    store8_nt(y + e, v);
   }
 }
 
@@ -486,8 +486,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const TD* dy, const 
     const int64_t r1 = min(M, r0 + rows_per_block);
     for (int64_t row = r0 + cm.r; row < r1; row += cm.rpp) {
       float xv[4], dv[4];
-      load4(x + row * ld + cm.chunk * 4, xv);
-      load4(dy + row * ld + cm.chunk * 4, dv);
+      load4_nt(x + row * ld + cm.chunk * 4, xv);
+      load4_nt(dy + row * ld + cm.chunk * 4, dv);
       const float rsc = row_scale ? row_scale[row / rpg] : 1.f;
 #pragma unroll
       for (int j = 0; j < 4; j += 2) {   // packed pairs (gelu_phi_pair_t)
@@ -560,24 +560,24 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const TD* dy, const TI* 
 #pragma unroll
       for (int i = 0; i < 2; ++i) o[j + i] = ww[j + i] * rs[j + i] * (gg[i] - k0[j + i] - xh[i] * k1[j + i]);
     }
-    store8(dx + e, o);
+    store8(dx + e, o);   // (read next by the branch GEMM: normal store, +1 % with nt)
   };
   int64_t row = r0 + cm.r;
   for (; row + cm.rpp < r1; row += 2 * cm.rpp) {
     const int64_t e0 = row * ld + cm.chunk * 8, e1 = e0 + (int64_t)cm.rpp * ld;
     float x0[8], d0[8], x1[8], d1[8];
-    load8(x + e0, x0);
-    load8(dy + e0, d0);
-    load8(x + e1, x1);
-    load8(dy + e1, d1);
+    load8_nt(x + e0, x0);
+    load8_nt(dy + e0, d0);
+    load8_nt(x + e1, x1);
+    load8_nt(dy + e1, d1);
     one(row, x0, d0);
     one(row + cm.rpp, x1, d1);
   }
   if (row < r1) {
     const int64_t e0 = row * ld + cm.chunk * 8;
     float x0[8], d0[8];
-    load8(x + e0, x0);
-    load8(dy + e0, d0);
+    load8_nt(x + e0, x0);
+    load8_nt(dy + e0, d0);
     one(row, x0, d0);
   }
 }
