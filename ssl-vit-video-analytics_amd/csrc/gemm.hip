@@ -1499,14 +1499,25 @@ bool pp_enabled() {
   }
   return pp_mode != 0;
 }
-// K <= 128 only: same-box A/B (profiles/r05b_gemm_persistent_ab.txt) -- the write-bound small-K
-// shapes gain 4-13 % (stage-0 expand 7.40 -> 6.46 ms, its BatchNorm-input data gradient 7.00 ->
-// 6.71), K = 256 / 384 are even, K = 768 / 1536 lose 9 %: persistent blocks drift apart, so the
-// n-tile blocks that share an A panel no longer stream it through L2 together.
+// Where it pays (same-box A/B, profiles/r05b_gemm_persistent_ab.txt, r05aa_gemm_pp_rounds.txt): K <= 128
+// (write-bound: stage-0 expand / projection data gradient -4..-13 %), and K <= 384 at N >= 512
+// (several n-tiles share each A panel: decoder qkv / fc1 forward -6..-7 %, fc2 data gradient
+// -2 %).  At K >= 768 it loses (fc1 / qkv data gradients +2..4 %), and with one n-tile (N = 96)
+// there is no A panel to share.  Blocks take at most pp_rounds() tiles each (8 at K <= 128, 2
+// above): fully persistent blocks drift apart, so the n-tile blocks that share an A panel no
+// longer stream it through L2 together (K = 384: -1..+1 % persistent against -6 % at 2 tiles).
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
 bool pp_ok(const GemmArgs& g) {
   return pp_enabled() && g.partial == nullptr && g.colsum == nullptr && !g.ctrans && !(g.epi & 4) &&
-         !((g.epi & 1) && g.aux) && g.aux_out == nullptr && g.K > 0 && g.K <= 2 * BKT && g.k_begin == 0 &&
-         g.k_chunk >= g.K;
+         !((g.epi & 1) && g.aux) && g.aux_out == nullptr && g.K > 0 && g.k_begin == 0 && g.k_chunk >= g.K &&
+         (g.K <= 2 * BKT || (g.K <= 6 * BKT && g.N >= 512));
+}
+int pp_rounds(const GemmArgs& g) {
+  static const int forced = env_int("SM_GEMM_PP_ROUNDS", -1);   // A/B runs; 0 = fully persistent
+  return forced >= 0 ? forced : g.K <= 2 * BKT ? 8 : 2;
 }
 template <bool BK, int IMP>
 bool launch_pp(const GemmArgs& g, hipStream_t st) {
@@ -1525,7 +1536,14 @@ bool launch_pp(const GemmArgs& g, hipStream_t st) {
   }
   const int64_t tiles = (int64_t)((g.N + 127) / 128) * ((g.M + 255) / 256);
   if (tiles <= slots) return false;   // one round: the one-tile-per-block form
-  hipLaunchKernelGGL((gemm_bf16_pp<BK, IMP>), dim3(slots), dim3(512), 0, st, g);
+  // at most R = pp_rounds() tiles per block (grid 8 ceil(T / 8 / R), at least one resident round)
+  const int rounds = pp_rounds(g);
+  int64_t grid = slots;
+  if (rounds > 0) {
+    const int64_t per = ((tiles + 7) / 8 + rounds - 1) / rounds;
+    if (8 * per > grid) grid = 8 * per;
+  }
+  hipLaunchKernelGGL((gemm_bf16_pp<BK, IMP>), dim3((unsigned)grid), dim3(512), 0, st, g);
   return true;
 }
 

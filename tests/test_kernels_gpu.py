@@ -841,22 +841,27 @@ def test_linear_dw_se_operand(Fr, HW, N, C, acc):
 
 
 @pytest.mark.parametrize("case", ["bias", "bias_unaligned", "gelu", "branch", "dx", "dx_res", "k128", "k40",
-                                  "stats"])
+                                  "stats", "k384", "k384_branch", "dx_k384", "stats_k192"])
 def test_gemm_persistent_bit_identical(case):
     """The persistent GEMM form (gemm_bf16_pp: tile epilogues written through LDS and stored
-    under the next tile's K loop; K <= 128) against the one-tile-per-block v2 form, bit for
-    bit: ragged M (a partial last m-tile) and N (392: a partial n-tile), K tails (96, 40: one
-    K-step), every epilogue option of the plain form (bias, GELU without side output, the
-    autocast-rounded branch + dropout + DropPath + residual), the data-gradient layout
-    (M/N-major B), and the BatchNorm-statistics epilogue.  > 512 tiles: the persistent path."""
+    under the next tile's K loop; K <= 128 at 8 tiles per block, K <= 384 with N >= 512 at 2)
+    against the one-tile-per-block v2 form, bit for bit: ragged M (a partial last m-tile) and
+    N (392 / 520: a partial n-tile), K tails (96, 40: one K-step; 384, 192: several), every
+    epilogue option of the plain form (bias, GELU without side output, the autocast-rounded
+    branch + dropout + DropPath + residual), the data-gradient layout (M/N-major B), and the
+    BatchNorm-statistics epilogue.  > 512 tiles: the persistent path."""
     kk = KK()
     M, N, Kd = 256 * 200 + 77, 392, 96
     if case == "k128":
         Kd = 128
     elif case == "k40":
         Kd = 40
+    elif case in ("k384", "k384_branch", "dx_k384"):
+        N, Kd = 520, 384
     elif case == "stats":
         M, N = 256 * 300 + 13, 384
+    elif case == "stats_k192":
+        M, N, Kd = 256 * 300 + 13, 768, 192
     x = rnd(M, Kd, dtype=torch.bfloat16, seed=310).to(DEV)
     w = rnd(N, Kd, dtype=torch.bfloat16, seed=311, scale=0.2).to(DEV)
     bias_buf = rnd(N + 1, seed=312).to(DEV)
@@ -865,18 +870,19 @@ def test_gemm_persistent_bit_identical(case):
     rs = (torch.rand(64, generator=torch.Generator().manual_seed(314)) * 2).to(DEV)
 
     def run():
-        if case in ("dx", "dx_res"):   # dX[M][Kd'] = dy[M][N] w[N][Kd']: here dy = x, w' = [Kd][N']
-            wt = rnd(Kd, 264, dtype=torch.bfloat16, seed=315, scale=0.2).to(DEV)
-            r2 = rnd(M, 264, dtype=torch.bfloat16, seed=316).to(DEV) if case == "dx_res" else None
+        if case in ("dx", "dx_res", "dx_k384"):   # dX[M][Kd'] = dy[M][N] w[N][Kd']: here dy = x, w' = [Kd][N']
+            n2 = 520 if case == "dx_k384" else 264
+            wt = rnd(Kd, n2, dtype=torch.bfloat16, seed=315, scale=0.2).to(DEV)
+            r2 = rnd(M, n2, dtype=torch.bfloat16, seed=316).to(DEV) if case == "dx_res" else None
             return (kk.linear_dx(x, wt, residual=r2),)
-        if case == "stats":
+        if case in ("stats", "stats_k192"):
             rm, rv = torch.zeros(N, device=DEV), torch.ones(N, device=DEV)
             nb = torch.zeros((), dtype=torch.int64, device=DEV)
             return kk.linear_bn_stats(x, w, rm, rv, 0.1, 1e-5, 1, nb) + (rm, rv)
         out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
         if case == "gelu":
             kk.gemm(x, w, out, M, N, Kd, 0, 0, Kd, Kd, N, bias=bias, gelu=True)
-        elif case == "branch":
+        elif case in ("branch", "k384_branch"):
             kk.gemm(x, w, out, M, N, Kd, 0, 0, Kd, Kd, N, bias=bias, beta=1.0, R=res, round_branch=True,
                     drop_p=0.1, seed=77, row_scale=rs, rows_per_group=M // 63)
         else:
@@ -892,7 +898,7 @@ def test_gemm_persistent_bit_identical(case):
         kk.gemm_persistent(prev)
     for a, b in zip(got, ref):
         assert torch.equal(a, b), case
-    if case == "bias":
+    if case in ("bias", "k384"):
         assert rel_err(got[0], x.float() @ w.float().t() + bias) < TOL[torch.bfloat16]
 
 
