@@ -53,7 +53,8 @@ def gemm(args):
     cases = [  # (name, M, N, K)
         ("dec fc1 fwd", B * 6272, 1536, 384), ("dec fc2 fwd", B * 6272, 384, 1536),
         ("dec qkv fwd", B * 6272, 1152, 384), ("s0 expand fwd", B * 8 * 12544, 384, 96),
-        ("s0 proj fwd", B * 8 * 12544, 96, 384), ("s2 fc1 fwd", B * 8 * 784, 1536, 384)]
+        ("s0 proj fwd", B * 8 * 12544, 96, 384), ("s2 fc1 fwd", B * 8 * 784, 1536, 384),
+        ("dec proj fwd", B * 6272, 384, 384), ("s1 qkv fwd", B * 8 * 3136, 576, 192)]
     for name, M, N, Kd in cases:
         if args.only and args.only not in name:
             continue

@@ -1511,9 +1511,10 @@ int env_int(const char* name, int dflt) {
   return e ? atoi(e) : dflt;
 }
 bool pp_ok(const GemmArgs& g) {
+  static const int pp_minn = env_int("SM_GEMM_PP_MINN", 512), pp_maxk = env_int("SM_GEMM_PP_MAXK", 6 * BKT);   // A/B
   return pp_enabled() && g.partial == nullptr && g.colsum == nullptr && !g.ctrans && !(g.epi & 4) &&
          !((g.epi & 1) && g.aux) && g.aux_out == nullptr && g.K > 0 && g.k_begin == 0 && g.k_chunk >= g.K &&
-         (g.K <= 2 * BKT || (g.K <= 6 * BKT && g.N >= 512));
+         (g.K <= 2 * BKT || (g.K <= pp_maxk && g.N >= pp_minn));
 }
 int pp_rounds(const GemmArgs& g) {
   static const int forced = env_int("SM_GEMM_PP_ROUNDS", -1);   // A/B runs; 0 = fully persistent
