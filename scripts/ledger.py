@@ -105,7 +105,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--top", type=int, default=60)
+    ap.add_argument("--arena", default="on", choices=["on", "off"],
+                    help="the device-memory arena, as bench.py's MAE step runs (its memory policy follows)")
     args = ap.parse_args()
+    if args.arena == "on":
+        from ssl_mae_amd import arena
+        arena.install()
     from ssl_mae_amd import kernels as K
     from ssl_mae_amd.build import build
     build()

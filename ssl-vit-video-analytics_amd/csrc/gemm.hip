@@ -1149,11 +1149,89 @@ SM_DEV __attribute__((always_inline)) void pp_stage(const GemmArgs& g, const f32
   }
 }
 
+// GELU with the pre-activation side output (fc1: y = drop(GELU(pre)), pre = bf16(acc + bias)
+// saved for the backward), no residual / row scale: pass 1 stages pre into the images and
+// leaves y in the accumulators in run order (acc[i][j][8p + e] = run (i, j, p) element e);
+// the images go to g.aux, then pp_stage_runs stages y for C -- the v2 epilogue's values and
+// roundings (gemm_epilogue: fma, epi & 2 rounding, GELU, keep mask), so bit-identical.
+SM_DEV __attribute__((always_inline)) void pp_stage_gelu_aux(const GemmArgs& g, f32x16 (&acc)[2][2], int m0, int n0,
+                                                             int wm, int wn, int l, char* img) {
+  const int h = l >> 5;
+  const uint32_t s32 = seed32(g.seed), thr = drop_thr(g.drop_p);
+  const float ks = g.drop_p > 0.f ? 1.f / (1.f - g.drop_p) : 1.f;
+  const auto brs = __builtin_amdgcn_make_buffer_rsrc((void*)g.bias, (short)0, g.bias ? g.N * 4 : 0, 0x00020000);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const RowStage rs_{img + i * 4096};
+    const int row = m0 + wm + 32 * i + (l & 31);
+    const uint32_t rb = drop_rowbase(s32, (uint64_t)row);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int col = n0 + wn + 32 * j + 16 * p + 8 * h;
+        float b8[8];
+        if (g.bias) {
+          const uint32_t o = col < g.N ? (uint32_t)col * 4u : BUF_OOB;
+          const float4 b0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(brs, o, 0, 0));
+          const float4 b1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(brs, o + 16, 0, 0));
+          b8[0] = b0.x; b8[1] = b0.y; b8[2] = b0.z; b8[3] = b0.w; b8[4] = b1.x; b8[5] = b1.y; b8[6] = b1.z; b8[7] = b1.w;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) b8[e] = 0.f;
+        }
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[i][j][8 * p + e]),
+                                                           __float_as_uint(acc[i][j][8 * p + 4 + e]), false, false);
+          v[e] = __uint_as_float(sw[0]);
+          v[4 + e] = __uint_as_float(sw[1]);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          v[e] = fmaf(v[e], g.alpha, b8[e]);
+          if (g.epi & 2) v[e] = (float)(__bf16)v[e];
+        }
+        stage_put<__bf16>(rs_, 0, j, p, h, l, v);   // pre
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = gelu_f(v[e]);
+        if (g.drop_p > 0.f) {
+#pragma unroll
+          for (int e4 = 0; e4 < 8; e4 += 4) {
+            const uint32_t hv = drop_hash(rb, (uint32_t)(col + e4));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e4 + e] *= ((hv >> (8 * e)) & 0xFFu) >= thr ? ks : 0.f;
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[i][j][8 * p + e] = v[e];
+      }
+  }
+}
+// y (run order in acc, pp_stage_gelu_aux) into the images
+SM_DEV __attribute__((always_inline)) void pp_stage_runs(const f32x16 (&acc)[2][2], int l, char* img) {
+  const int h = l >> 5;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const RowStage rs_{img + i * 4096};
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = acc[i][j][8 * p + e];
+        stage_put<__bf16>(rs_, 0, j, p, h, l, v);
+      }
+  }
+}
+
 // The wave's two images -> C by unconditional buffer stores (RowStage::flush's order and
 // statistics); rows past M are dropped by the descriptor, columns past N by the offset.
 template <bool STATS>
-SM_DEV __attribute__((always_inline)) void pp_flush(const GemmArgs& g, int m0, int n0, int wm, int wn, int l,
-                                                    const char* img) {
+SM_DEV __attribute__((always_inline)) void pp_flush(const GemmArgs& g, const void* out, int m0, int n0, int wm, int wn,
+                                                    int l, const char* img) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's image writes
   const int c = l & 7;
   const int col = n0 + wn + 8 * c;
@@ -1165,7 +1243,7 @@ SM_DEV __attribute__((always_inline)) void pp_flush(const GemmArgs& g, int m0, i
   for (int i = 0; i < 2; ++i) {
     const int r0 = m0 + wm + 32 * i;
     const int rows_valid = g.M - r0;
-    const auto rs = rows_rsrc((const __bf16*)g.C + (int64_t)r0 * g.ldc, rows_valid, g.ldc * 2);
+    const auto rs = rows_rsrc((const __bf16*)out + (int64_t)r0 * g.ldc, rows_valid, g.ldc * 2);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int r = (l >> 3) + 8 * q;
@@ -1192,13 +1270,14 @@ SM_DEV __attribute__((always_inline)) void pp_flush(const GemmArgs& g, int m0, i
 }
 
 // K-major A; B K-major (forward, y = x W^T) or M/N-major (data gradient, dX = dy W); bf16
-// output; IMP 0 plain / 8 output BatchNorm statistics.  No split-K (k_begin = 0, k_chunk >=
+// output; IMP 0 plain / 8 output BatchNorm statistics / 13 GELU with the pre-activation side
+// output (pp_stage_gelu_aux).  No split-K (k_begin = 0, k_chunk >=
 // K).  Grid: a multiple of 8 blocks, at most T / 8 per XCD group; block b serves group b & 7
 // (its tiles are a contiguous m-major range, so concurrently running blocks share A panels in
 // the XCD's L2) and walks tiles b >> 3, + gridDim.x / 8, ... of it.
 template <bool BK, int IMP>
 __global__ __launch_bounds__(512, 4) void gemm_bf16_pp(GemmArgs g) {
-  static_assert(IMP == 0 || IMP == 8, "persistent form: plain or statistics epilogue");
+  static_assert(IMP == 0 || IMP == 8 || IMP == 13, "persistent form: plain, statistics or GELU + pre epilogue");
   constexpr int BMV = 256, BNV = 128, NT = 512;
   constexpr int CHA = TileLoader<BMV, NT, true>::CH, CHB = TileLoader<BNV, NT, BK>::CH;
   constexpr int KSTEPB = TileLoader<BNV, NT, BK>::KSTEP;
@@ -1317,17 +1396,28 @@ __global__ __launch_bounds__(512, 4) void gemm_bf16_pp(GemmArgs g) {
   ksteps();
   int cm0 = lm0, cn0 = ln0;
   for (int in = it + qstep; in < cnt; in += qstep) {
-    pp_stage(g, acc, cm0, cn0, wm, wn, opaque_tid() & 63, img);
+    if constexpr (IMP == 13) pp_stage_gelu_aux(g, acc, cm0, cn0, wm, wn, opaque_tid() & 63, img);
+    else pp_stage(g, acc, cm0, cn0, wm, wn, opaque_tid() & 63, img);
     setup(in);
     issue(0);
-    pp_flush<IMP == 8>(g, cm0, cn0, wm, wn, opaque_tid() & 63, img);
+    if constexpr (IMP == 13) {   // pre -> aux (stores younger than the next operands), then y
+      pp_flush<false>(g, g.aux, cm0, cn0, wm, wn, opaque_tid() & 63, img);
+      pp_stage_runs(acc, opaque_tid() & 63, img);
+    }
+    pp_flush<IMP == 8>(g, g.C, cm0, cn0, wm, wn, opaque_tid() & 63, img);
     __syncthreads();   // every wave's images read before the next tile's operands land
     cm0 = lm0;
     cn0 = ln0;
     ksteps();
   }
-  pp_stage(g, acc, cm0, cn0, wm, wn, threadIdx.x & 63, img);
-  pp_flush<IMP == 8>(g, cm0, cn0, wm, wn, threadIdx.x & 63, img);
+  if constexpr (IMP == 13) {
+    pp_stage_gelu_aux(g, acc, cm0, cn0, wm, wn, threadIdx.x & 63, img);
+    pp_flush<false>(g, g.aux, cm0, cn0, wm, wn, threadIdx.x & 63, img);
+    pp_stage_runs(acc, threadIdx.x & 63, img);
+  } else {
+    pp_stage(g, acc, cm0, cn0, wm, wn, threadIdx.x & 63, img);
+  }
+  pp_flush<IMP == 8>(g, g.C, cm0, cn0, wm, wn, threadIdx.x & 63, img);
 }
 
 // ============================================================ f32 MFMA kernel
@@ -1513,7 +1603,8 @@ int env_int(const char* name, int dflt) {
 bool pp_ok(const GemmArgs& g) {
   static const int pp_minn = env_int("SM_GEMM_PP_MINN", 512), pp_maxk = env_int("SM_GEMM_PP_MAXK", 6 * BKT);   // A/B
   return pp_enabled() && g.partial == nullptr && g.colsum == nullptr && !g.ctrans && !(g.epi & 4) &&
-         !((g.epi & 1) && g.aux) && g.aux_out == nullptr && g.K > 0 && g.k_begin == 0 && g.k_chunk >= g.K &&
+         (!((g.epi & 1) && g.aux) || (g.beta == 0.f && g.row_scale == nullptr)) && g.aux_out == nullptr &&
+         g.K > 0 && g.k_begin == 0 && g.k_chunk >= g.K &&
          (g.K <= 2 * BKT || (g.K <= pp_maxk && g.N >= pp_minn));
 }
 int pp_rounds(const GemmArgs& g) {
@@ -1554,7 +1645,13 @@ void launch_bf16(const GemmArgs& g, int splits, hipStream_t st) {
   const int bm = variant_bm(v), bn = variant_bn(v);
   const int tiles = ((g.N + bn - 1) / bn) * ((g.M + bm - 1) / bm);
   if constexpr (AK && VEC && sizeof(TC) == 2) {
-    if (v == 2 && splits == 1 && pp_ok(g) && launch_pp<BK, 0>(g, st)) return;
+    if (v == 2 && splits == 1 && pp_ok(g)) {
+      if ((g.epi & 1) && g.aux) {   // fc1: GELU + pre-activation side output
+        if (launch_pp<BK, 13>(g, st)) return;
+      } else if (launch_pp<BK, 0>(g, st)) {
+        return;
+      }
+    }
   }
   if (v == 1) hipLaunchKernelGGL((gemm_bf16_kernel<AK, BK, TC, VEC>), dim3(tiles, 1, splits), dim3(256), 0, st, g);
   else if (v == 2) hipLaunchKernelGGL((gemm_bf16_v2<AK, BK, TC, VEC, 256>), dim3(tiles * splits), dim3(512), 0, st, g);
