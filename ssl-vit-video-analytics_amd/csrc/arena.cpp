@@ -45,6 +45,7 @@ struct Block {
 
 struct Arena {
   bool tried = false;
+  bool attached = false;   // sm_arena_attach (host-memory tests): report exhaustion as nullptr
   char* base = nullptr;
   size_t cap = 0;
   bool home_set = false;
@@ -167,7 +168,13 @@ void* sm_arena_alloc(ssize_t size, int device, hipStream_t stream) {
       std::fprintf(stderr, "[sm_arena] device %d: %zu B do not fit (in use %zu of %zu B); using hipMalloc\n",
                    device, n, a.in_use, a.cap);
   }
-  return foreign_alloc(a, n);
+  if (void* p = foreign_alloc(a, n)) return p;
+  if (a.attached) return nullptr;
+  // PyTorch's pluggable-allocator hook does not check for null: a null block would reach a
+  // kernel as a device address.  Stop here with the numbers instead.
+  std::fprintf(stderr, "[sm_arena] device %d: out of device memory for %zu B (arena in use %zu of %zu B, %zu B outside)\n",
+               device, n, a.in_use, a.cap, [&] { size_t t = 0; for (const auto& kv : a.foreign) t += kv.second; return t; }());
+  std::abort();
 }
 
 void sm_arena_free(void* ptr, ssize_t size, int device, hipStream_t stream) {
@@ -218,6 +225,7 @@ int sm_arena_attach(int device, void* base, uint64_t cap) {
   Arena& a = g_arena[device];
   if (a.tried) return -1;
   a.tried = true;
+  a.attached = true;
   a.base = static_cast<char*>(base);
   a.cap = cap / kAlign * kAlign;
   a.blocks[0] = Block{a.cap, true};
