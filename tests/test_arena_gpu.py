@@ -16,6 +16,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def _run(mode):
+    try:   # this process's cached blocks back to the device before the child takes its heap
+        import torch
+        if torch.cuda.is_initialized():
+            torch.cuda.empty_cache()
+    except Exception:
+        pass
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -31,7 +37,7 @@ def test_arena_step_matches_caching_allocator():
     a = _run("arena")
     c = _run("caching")
     st = a["arena"]
-    assert st["capacity"] > 100 * 2 ** 30 and st["requests"] > 100
+    assert st["capacity"] > 16 * 2 ** 30 and st["requests"] > 100
     assert st["hipmalloc_requests"] == 0 and st["outside_bytes"] == 0
     assert 0 < st["peak"] <= st["capacity"]
     assert a["launched"] == c["launched"] == 0                 # every bucket reduced and the hook reset
