@@ -1,5 +1,5 @@
 """Before/after SQ-counter table from two scripts/pmc_kernel.sh-style pass sets:
-    python scripts/pmc_ab_table.py gpurun_out/TAG_a gpurun_out/TAG_b KERNEL_FILTER [label_a label_b]
+    python scripts/pmc_ab_table.py gpurun_out/TAG_a gpurun_out/TAG_b KERNEL_FILTER[||FILTER_B] [label_a label_b]
 Per dispatch: wave cycles, waits as a share of wave cycles, VALU / LDS / MFMA work."""
 import collections
 import csv
@@ -20,7 +20,8 @@ def load(tag, flt):
 
 a, b, flt = sys.argv[1], sys.argv[2], sys.argv[3]
 la, lb = (sys.argv[4], sys.argv[5]) if len(sys.argv) > 5 else ("before", "after")
-A, B = load(a, flt), load(b, flt)
+fa, fb = flt.split("||") if "||" in flt else (flt, flt)   # "A||B": different kernel names per arm
+A, B = load(a, fa), load(b, fb)
 rows = [("SQ_WAVE_CYCLES", None), ("SQ_WAIT_ANY", "SQ_WAVE_CYCLES"), ("SQ_WAIT_INST_ANY", "SQ_WAVE_CYCLES"),
         ("SQ_ACTIVE_INST_ANY", "SQ_WAVE_CYCLES"), ("SQ_ACTIVE_INST_VALU", "SQ_WAVE_CYCLES"),
         ("SQ_WAIT_INST_LDS", "SQ_WAVE_CYCLES"), ("SQ_VALU_MFMA_BUSY_CYCLES", None), ("SQ_BUSY_CYCLES", None),
