@@ -1609,7 +1609,8 @@ bool pp_ok(const GemmArgs& g) {
 }
 int pp_rounds(const GemmArgs& g) {
   static const int forced = env_int("SM_GEMM_PP_ROUNDS", -1);   // A/B runs; 0 = fully persistent
-  return forced >= 0 ? forced : g.K <= 2 * BKT ? 8 : 2;
+  static const int small_k = env_int("SM_GEMM_PP_ROUNDS_SMALLK", 8), mid_k = env_int("SM_GEMM_PP_ROUNDS_MIDK", 2);
+  return forced >= 0 ? forced : g.K <= 2 * BKT ? small_k : mid_k;
 }
 template <bool BK, int IMP>
 bool launch_pp(const GemmArgs& g, hipStream_t st) {
