@@ -56,8 +56,10 @@ struct Arena {
   size_t in_use = 0, peak = 0, n_alloc = 0, n_foreign = 0, n_oom = 0;
 };
 
-Arena g_arena[kMaxDevices];
-std::mutex g_mu;
+// Never destroyed: PyTorch can release blocks from its own static destructors, which may run
+// after this library's at process exit.
+Arena* const g_arena = new Arena[kMaxDevices];
+std::mutex& g_mu = *new std::mutex;
 
 size_t env_reserve() {
   const char* s = std::getenv("SM_ARENA_RESERVE_MIB");
