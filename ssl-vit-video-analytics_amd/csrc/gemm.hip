@@ -1270,14 +1270,19 @@ SM_DEV __attribute__((always_inline)) void pp_flush(const GemmArgs& g, const voi
 }
 
 // K-major A; B K-major (forward, y = x W^T) or M/N-major (data gradient, dX = dy W); bf16
-// output; IMP 0 plain / 8 output BatchNorm statistics / 13 GELU with the pre-activation side
-// output (pp_stage_gelu_aux).  No split-K (k_begin = 0, k_chunk >=
+// output; IMP 0 plain / 8 output BatchNorm statistics / 11, 12 BatchNorm-input A operand with /
+// without the statistics (v2's IMP 11 / 12 transform in put()) / 13 GELU with the
+// pre-activation side output (pp_stage_gelu_aux).  No split-K (k_begin = 0, k_chunk >=
 // K).  Grid: a multiple of 8 blocks, at most T / 8 per XCD group; block b serves group b & 7
 // (its tiles are a contiguous m-major range, so concurrently running blocks share A panels in
 // the XCD's L2) and walks tiles b >> 3, + gridDim.x / 8, ... of it.
 template <bool BK, int IMP>
 __global__ __launch_bounds__(512, 4) void gemm_bf16_pp(GemmArgs g) {
-  static_assert(IMP == 0 || IMP == 8 || IMP == 13, "persistent form: plain, statistics or GELU + pre epilogue");
+  static_assert(IMP == 0 || IMP == 8 || IMP == 11 || IMP == 12 || IMP == 13,
+                "persistent form: plain, statistics, BatchNorm-input (+ statistics) or GELU + pre epilogue");
+  constexpr bool STATS = IMP == 8 || IMP == 11;
+  constexpr bool XA = IMP == 11 || IMP == 12;   // A = bf16(a sc + sh) formed on its way to LDS (as v2)
+  __shared__ float xtab[XA ? 2 * XB_MAXK : 4];
   constexpr int BMV = 256, BNV = 128, NT = 512;
   constexpr int CHA = TileLoader<BMV, NT, true>::CH, CHB = TileLoader<BNV, NT, BK>::CH;
   constexpr int KSTEPB = TileLoader<BNV, NT, BK>::KSTEP;
@@ -1295,6 +1300,14 @@ __global__ __launch_bounds__(512, 4) void gemm_bf16_pp(GemmArgs g) {
   const int cnt = T8 + (x < R8 ? 1 : 0), tbase = x * T8 + (x < R8 ? x : R8);
   const int it = blockIdx.x >> 3;
   if (it >= cnt) return;
+  if constexpr (XA) {   // = Affine8::init per channel (v2's IMP 11 / 12 table)
+    for (int c = threadIdx.x; c < g.K; c += NT) {
+      const float sc = g.xb_act.rstd[c] * g.xb_act.w[c];
+      xtab[c] = sc;
+      xtab[XB_MAXK + c] = bn_shift(g.xb_act.b[c], g.xb_act.mean[c], sc);
+    }
+    __syncthreads();
+  }
   const __bf16* A = (const __bf16*)g.A;
   const __bf16* B = (const __bf16*)g.B;
   const int K = g.K;
@@ -1341,8 +1354,26 @@ __global__ __launch_bounds__(512, 4) void gemm_bf16_pp(GemmArgs g) {
                                               rsb, (bc < bcols && bk + KSTEPB * i < kv) ? b_v : BUF_OOB, i * b_rs, 0));
     }
   };
-  auto put = [&]() {
+  auto put = [&](int k0) {
     const int t = opaque_tid();
+    if constexpr (XA) {   // x = bf16(a sc + sh) of the thread's 8 channels (chunks past K stay zero)
+      const int c0 = k0 + (t & 7) * 8;
+      if (c0 < K) {
+#pragma unroll
+        for (int jp = 0; jp < 4; ++jp) {
+          const float2 sc2 = *(const float2*)(xtab + c0 + 2 * jp);
+          const float2 sh2 = *(const float2*)(xtab + XB_MAXK + c0 + 2 * jp);
+#pragma unroll
+          for (int i = 0; i < CHA; ++i) {
+            uint32_t* wv = (uint32_t*)&ra[i];
+            const float lo = __uint_as_float(wv[jp] << 16), hi = __uint_as_float(wv[jp] & 0xFFFF0000u);
+            typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+            const bf16x2 o = {(__bf16)fmaf(lo, sc2.x, sh2.x), (__bf16)fmaf(hi, sc2.y, sh2.y)};
+            wv[jp] = __builtin_bit_cast(uint32_t, o);
+          }
+        }
+      }
+    }
     const int a_l0 = kmaj_off(t >> 3, t & 7);
     const int b_l0 = BK ? a_l0 : mnmaj_off_r<BNV>(t / (BNV / 8), (t % (BNV / 8)) * 8);
 #pragma unroll
@@ -1378,13 +1409,13 @@ __global__ __launch_bounds__(512, 4) void gemm_bf16_pp(GemmArgs g) {
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    put();   // K-step 0, outside the loop (see above)
+    put(0);   // K-step 0, outside the loop (see above)
     __syncthreads();
     if (nk > 1) issue(BKT);
     kstep();
     __syncthreads();
     for (int ks = 1; ks < nk; ++ks) {
-      put();
+      put(ks * BKT);
       __syncthreads();
       if (ks + 1 < nk) issue((ks + 1) * BKT);
       kstep();
@@ -1404,7 +1435,7 @@ __global__ __launch_bounds__(512, 4) void gemm_bf16_pp(GemmArgs g) {
       pp_flush<false>(g, g.aux, cm0, cn0, wm, wn, opaque_tid() & 63, img);
       pp_stage_runs(acc, opaque_tid() & 63, img);
     }
-    pp_flush<IMP == 8>(g, g.C, cm0, cn0, wm, wn, opaque_tid() & 63, img);
+    pp_flush<STATS>(g, g.C, cm0, cn0, wm, wn, opaque_tid() & 63, img);
     __syncthreads();   // every wave's images read before the next tile's operands land
     cm0 = lm0;
     cn0 = ln0;
@@ -1417,7 +1448,7 @@ __global__ __launch_bounds__(512, 4) void gemm_bf16_pp(GemmArgs g) {
   } else {
     pp_stage(g, acc, cm0, cn0, wm, wn, threadIdx.x & 63, img);
   }
-  pp_flush<IMP == 8>(g, g.C, cm0, cn0, wm, wn, threadIdx.x & 63, img);
+  pp_flush<STATS>(g, g.C, cm0, cn0, wm, wn, threadIdx.x & 63, img);
 }
 
 // ============================================================ f32 MFMA kernel
@@ -2098,6 +2129,12 @@ static int linear_bnin_launch(int M, int N, int K, const void* a, const float* m
   g.xb_act = ChanAffine{mean, rstd, bw, bb, 0};
   g.stat_part = stat_part;
   const int tiles_n = (N + 127) / 128;
+  if (gemm_variant(M, N, K) == 2 && pp_ok(g)) {   // persistent form (K <= 128: the stage-0 expand)
+    if (stat_part ? launch_pp<true, 11>(g, stream) : launch_pp<true, 12>(g, stream)) {
+      SM_CHECK_LAUNCH();
+      return 0;
+    }
+  }
   if (gemm_variant(M, N, K) == 2) {
     const dim3 grid(tiles_n * ((M + 255) / 256));
     if (stat_part) hipLaunchKernelGGL((gemm_bf16_v2<true, true, __bf16, true, 256, 11>), grid, dim3(512), 0, stream, g);

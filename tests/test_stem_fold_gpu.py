@@ -46,8 +46,11 @@ def _rnd(*shape, seed, scale=1.0):
     return (torch.randn(*shape, generator=g) * scale).to(torch.bfloat16).to(DEV)
 
 
-@pytest.mark.parametrize("M,N,K", [(2 * 12544, 384, 96), (1000, 384, 96), (300, 40, 24), (130, 136, 256)])
+@pytest.mark.parametrize("M,N,K", [(2 * 12544, 384, 96), (1000, 384, 96), (300, 40, 24), (130, 136, 256),
+                                   (48 * 12544 + 77, 384, 96), (256 * 300 + 13, 520, 192)])
 def test_linear_bnin_bit_identical(M, N, K):
+    """(the last two: > 512 tiles -- the persistent GEMM form, ragged M; K = 96 at 8 tiles per block,
+    K = 192 with N >= 512 at 2)"""
     kk = KK()
     a = _rnd(M, K, seed=1, scale=2.0)
     w = _rnd(N, K, seed=2, scale=0.2)
