@@ -304,8 +304,9 @@ class TinyViT(nn.Module):
 _PEAK_GIB_PER_FRAME = {
     # (0, 1, 2): stage 0 resident too, 2 x 131.9 GiB at B = 128 less the B-independent 0.7 GiB
     ((2, 2, 6, 2), 4): {(0, 1, 2): 263.1 / 2048, (1, 2): 216.0 / 2048, (2,): 171.9 / 2048, (): 143.6 / 2048},
-    # C3 ViT-Small (depths 2,2,12,2 + 8-layer decoder): (2,) and (1, 2) exceed 288 GB at B=256
-    ((2, 2, 12, 2), 8): {(): 184.0 / 2048},
+    # C3 ViT-Small (depths 2,2,12,2 + 8-layer decoder): (2,) and (1, 2) exceed 288 GB at B=256;
+    # (0,) (stage 0 resident, arena only) 231.2 GiB, +3.2 % (profiles/r05ap_small_stage0_resident.txt)
+    ((2, 2, 12, 2), 8): {(0,): 231.2 / 2048, (): 184.0 / 2048},
 }
 
 
@@ -322,7 +323,7 @@ def auto_resident_stages(frames, image_size, bf16, device, budget=0.85, key=((2,
         return ()
     total = torch.cuda.get_device_properties(device).total_memory / 2 ** 30
     scale = frames * (image_size / 224.0) ** 2 * (1 if bf16 else 2)
-    for policy in ((0, 1, 2), (1, 2), (2,)):
+    for policy in ((0, 1, 2), (1, 2), (2,), (0,)):
         if policy not in table:
             continue
         if 0 in policy:

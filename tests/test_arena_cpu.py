@@ -104,3 +104,19 @@ def test_stage0_resident_policy_needs_arena(monkeypatch, policy_cap, expect):
     monkeypatch.setattr(arena, "capacity_gib", lambda d=None: policy_cap)
     assert TV.auto_resident_stages(256 * 8, 224, True, "cuda") == expect
     assert TV.auto_lite_stages(256 * 8, 224, True, "cuda", expect) == ((0,) if expect == (1, 2) else ())
+
+
+@pytest.mark.parametrize("cap, expect", [(0.0, ()), (281.0, (0,))])
+def test_small_stage0_resident_needs_arena(monkeypatch, cap, expect):
+    """C3 ViT-Small (depths 2,2,12,2 + 8-layer decoder): stage 0 resident (231.2 GiB at B = 256)
+    only under the arena; its other resident policies do not fit 288 GB."""
+    import torch
+    from ssl_mae_amd import tiny_vit as TV
+
+    class Props:
+        total_memory = 288 * 2 ** 30
+    monkeypatch.setattr(torch.cuda, "get_device_properties", lambda d: Props())
+    monkeypatch.setattr(arena, "active", lambda: cap > 0)
+    monkeypatch.setattr(arena, "capacity_gib", lambda d=None: cap)
+    assert TV.auto_resident_stages(256 * 8, 224, True, "cuda", key=((2, 2, 12, 2), 8)) == expect
+    assert TV.auto_lite_stages(256 * 8, 224, True, "cuda", expect, key=((2, 2, 12, 2), 8)) == ()
