@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--size", type=int, default=224)
     ap.add_argument("--mask-ratio", type=float, default=0.75)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-calibration", action="store_true",
+                    help="skip the box calibration (bare MFMA loops + a 4.9 GB copy) before the timed steps")
     ap.add_argument("--resident", default="",
                     help="encoder stages kept resident in HBM (no checkpoint recompute): "
                          "comma list, or 'none'; default: the model's auto policy")
@@ -66,44 +68,85 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(T, S, ratio, B=1):
-    """The CPU oracle (fp32 restatement of the reference path) timed on the host
-    cores: one fwd+bwd+AdamW step of the reference's C1 step (train_ssl_mae.py:66-91,
-    T=8, 224^2) on B = 1 clip (a bounded sample: the reference's own C1 batch of 4 takes
-    ~2 min on 8 cores), with dropout / DropPath on as the reference ships them (attention
-    probabilities materialised per head, as nn.MultiheadAttention's math path), after an
-    untimed small warm-up step (thread pool, allocator); torch's threads = the box's CPU
-    share (OMP_NUM_THREADS).  ~20-40 s."""
+def cpu_baseline(T, S, ratio, sweep=((1, 16), (1, 64), (4, None))):
+    """The CPU oracle (fp32 restatement of the reference path, oracle/mae_oracle.py) timed on
+    the GPU box's host cores: one fwd+bwd+AdamW step of the reference's C1 step
+    (train_ssl_mae.py:66-91, T=8, 224^2) per (clips, threads) point of `sweep` (None = every
+    CPU of the process's affinity set), with dropout / DropPath on as the reference ships them
+    (attention probabilities materialised per head, as nn.MultiheadAttention's math path),
+    after an untimed small warm-up step per thread count.  The headline value is the
+    reference's own C1 batch (B = 4) on all affinity CPUs; the B = 1 points show the thread
+    scaling at 16 (the box's default OMP share) and 64 threads.  ~40-60 s in total."""
     from oracle import mae_oracle as O
     from ssl_mae_amd.init_rule import param_value, synthetic_clip
     cfg = {"dataset": {"clip_len": T, "image_size": S},
            "model": {"decoder_embed_dim": 384, "decoder_depth": 4, "decoder_num_heads": 6},
            "ssl": {"mask_ratio": ratio, "norm_pix_loss": True}, "train_dropout": True}
-    threads = torch.get_num_threads()
     try:
         affinity = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
-        affinity = None
-    P = O.make_params(cfg, param_value)
-    bufs = O.init_buffers(P)
-    opt = O.AdamWState(lr=5e-4)
-    torch.manual_seed(42)
+        affinity = os.cpu_count()
+    threads0 = torch.get_num_threads()
     wcfg = dict(cfg, dataset={"clip_len": 2, "image_size": 64})
-    wP = O.make_params(wcfg, param_value)
-    O.train_step(wP, O.init_buffers(wP), O.AdamWState(lr=5e-4), torch.from_numpy(synthetic_clip(1, 2, 64, seed=6)),
-                 O.get_tube_mask(1, 2, 64, ratio), wcfg)   # warm-up (small)
-    del wP
-    clip = torch.from_numpy(synthetic_clip(B, T, S, seed=7))
-    mask = O.get_tube_mask(B, T, (S // 8) ** 2, ratio)
-    t0 = time.perf_counter()
-    O.train_step(P, bufs, opt, clip, mask, cfg)
-    dt = time.perf_counter() - t0
-    return {"value": round(B / dt, 5), "unit": "clips/s", "cores": threads, "threads": threads,
-            "nproc": os.cpu_count(), "affinity_cpus": affinity, "kind": "port",
-            "sample": f"BASELINE config 1 step shape on {B} clip ({T}x3x{S}x{S}): one fp32 fwd+bwd+AdamW step of "
-                      f"oracle/mae_oracle.py with dropout / DropPath on (as the reference), after a small "
-                      f"warm-up step, on {threads} torch threads (the box's CPU share; nproc "
-                      f"{os.cpu_count()}, affinity {affinity}); {dt:.1f} s"}
+    points = []
+    try:
+        for B, th in sweep:
+            th = affinity if th is None else min(th, affinity)
+            torch.set_num_threads(th)
+            torch.manual_seed(42)
+            wP = O.make_params(wcfg, param_value)
+            O.train_step(wP, O.init_buffers(wP), O.AdamWState(lr=5e-4),
+                         torch.from_numpy(synthetic_clip(1, 2, 64, seed=6)), O.get_tube_mask(1, 2, 64, ratio), wcfg)
+            del wP
+            P = O.make_params(cfg, param_value)
+            bufs = O.init_buffers(P)
+            opt = O.AdamWState(lr=5e-4)
+            clip = torch.from_numpy(synthetic_clip(B, T, S, seed=7))
+            mask = O.get_tube_mask(B, T, (S // 8) ** 2, ratio)
+            t0 = time.perf_counter()
+            O.train_step(P, bufs, opt, clip, mask, cfg)
+            dt = time.perf_counter() - t0
+            points.append({"clips": B, "threads": th, "s_per_step": round(dt, 2), "clips_per_s": round(B / dt, 5)})
+            del P, bufs, opt
+    finally:
+        torch.set_num_threads(threads0)
+    head = points[-1]
+    return {"value": head["clips_per_s"], "unit": "clips/s", "cores": head["threads"], "threads": head["threads"],
+            "nproc": os.cpu_count(), "affinity_cpus": affinity, "kind": "port", "sweep": points,
+            "sample": f"BASELINE config 1 step: one fp32 fwd+bwd+AdamW step of oracle/mae_oracle.py on {head['clips']} "
+                      f"clips ({T}x3x{S}x{S}) with dropout / DropPath on (as the reference), after a small warm-up "
+                      f"step, on {head['threads']} torch threads = every CPU of the process's affinity set (nproc "
+                      f"{os.cpu_count()}); 'sweep' adds 1-clip steps at 16 and 64 threads; {head['s_per_step']} s"}
+
+
+def calibration(dev, copy_gb=4.9):
+    """Box calibration before the timed steps (~2 s): bare bf16 MFMA loops on random register
+    data in both shapes (csrc/calib.hip; TFLOP/s and the in-kernel clock, MI355X_MICROARCH.md
+    'DVFS give-back' items 5-7: devices differ by up to 12 % on the same MFMA loop) and a
+    device-to-device copy of `copy_gb` GB (read + write bytes / time), so a line from a slow box
+    can be told from slow code."""
+    from ssl_mae_amd import kernels as K
+    out = {}
+    for shape, name in ((32, "32x32x16"), (16, "16x16x32")):
+        tf, mhz, ms = K.calibrate_mfma(shape, iters=1_500_000)
+        out[f"mfma_{name}_tflops"] = round(tf, 1)
+        out[f"mfma_{name}_clock_mhz"] = round(mhz) if mhz else None
+        out[f"mfma_{name}_ms"] = round(ms, 1)
+    n = int(copy_gb * 1e9) // 4
+    src = torch.empty(n, dtype=torch.float32, device=dev).uniform_()
+    dst = torch.empty_like(src)
+    dst.copy_(src)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(3):
+        dst.copy_(src)
+    e.record()
+    e.synchronize()
+    ms = s.elapsed_time(e) / 3
+    out["copy_gbs"] = round(2 * n * 4 / (ms * 1e-3) / 1e9, 1)
+    out["copy_gb"] = copy_gb
+    del src, dst
+    return out
 
 
 PROBE_KERNELS = {"dec_attn_fwd": "attn_fwd_bf16<64, true>",
@@ -272,8 +315,14 @@ def main():
         loss, _, _ = train_step(model, clips[i % 2], opt, scaler, ssl_cfg, bf16=True)
         return loss
 
+    if args.resident or args.lite:   # an explicit policy must fit before the first step (RuntimeError)
+        enc = model.encoder
+        TV.check_memory_policy(B * T, S, True, dev, resident_used(model, B * T, S), lite_used(model, B * T, S),
+                               key=(tuple(enc.depths), enc._sm_dec_depth))
     for i in range(args.warmup):
         step(i)
+    torch.cuda.synchronize()
+    calib = calibration(dev) if not args.no_calibration else None
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -281,11 +330,12 @@ def main():
     probe.active = True
     stem_probe.active = True
     t0 = time.perf_counter()
-    loss_vals = []
+    loss_vals, step_end = [], []
     for i in range(args.steps):
         # the reference syncs on the loss every step (total_loss += loss.item(),
         # train_ssl_mae.py:91): so does the timed loop
         loss_vals.append(float(step(i).item()))
+        step_end.append(time.perf_counter())
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     probe.active = False
@@ -349,6 +399,7 @@ def main():
                 cpu = cpu_baseline(T, S, r)
             except Exception as e:  # the baseline must not kill the bench line
                 cpu = {"value": None, "error": repr(e)[:200]}
+        step_ms = [round((b_ - a_) * 1e3, 1) for a_, b_ in zip([t0] + step_end[:-1], step_end)]
         line = {
             "metric": METRIC, "value": round(value, 3), "unit": "clips/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 2),
@@ -363,7 +414,10 @@ def main():
                        "per_gpu_batch": B, "frames": T, "image_size": S, "mask_ratio": r,
                        "parallelism": f"dp{world}",
                        "resident_stages": list(resident_used(model, B * T, S)),
-                       "lite_stages": lite_used(model, B * T, S)},
+                       "lite_stages": lite_used(model, B * T, S),
+                       **({"gemm_tuning": K.gemm_tuning_nondefault()} if K.gemm_tuning_nondefault() else {})},
+            "calibration": calib,
+            "step_ms_first5": step_ms[:5], "step_ms_last5": step_ms[-5:],
             "roofline": roof,
             "model_tflops_per_gpu": round(step_tflops, 1) if step_tflops else None,
             "model_mfu": round(step_tflops / MFMA_BF16_PEAK_TFLOPS, 4) if step_tflops else None,

@@ -42,10 +42,17 @@ int sm_gemm(int ab_dtype, int c_dtype, int a_layout, int b_layout, int M, int N,
             void* workspace, int64_t ws_bytes, hipStream_t stream);
 /* Form of the non-split bf16 GEMMs with a K-major A and a plain bf16 epilogue (every
  * forward / data-gradient Linear of the step): 1 = persistent blocks with each tile's
- * output stores drained under the next tile's K loop (default; SM_GEMM_PP=0 in the
- * environment starts the process with 0), 0 = one tile per block.  Outputs are
- * bit-identical either way.  mode < 0 only queries.  Returns the previous mode. */
+ * output stores drained under the next tile's K loop (default), 0 = one tile per block.
+ * Outputs are bit-identical either way.  mode < 0 only queries.  Returns the previous mode.
+ * (= sm_gemm_tuning key 1.) */
 int sm_gemm_persistent(int mode);
+/* GEMM dispatch tuning for A/B measurement scripts (never changed by the product path):
+ * key 0 tile variant (0 = per-shape rule, 1-3 pinned), 1 persistent form on/off,
+ * 2 / 3 persistent form's minimum N / maximum K at K > 128, 4 tiles per persistent block
+ * (-1 = per-K rule, 0 = fully persistent), 5 / 6 tiles per block at K <= 128 / above.
+ * *prev <- the current value; set > 0 stores value, set < 0 restores the default.
+ * Returns 0, or -2 for an unknown key.  Host-side only (no launch). */
+int sm_gemm_tuning(int key, int set, int value, int* prev);
 /* Weight + bias gradient of y = x W^T + b (Linear / 1x1 conv backward, e.g.
  * tiny_vit.py:74-84 Mlp, mae_vit_adapter.py:40-48 decoder layers): dW[nout][nin]
  * (+)= dy^T x and db[nout] += sum_rows dy in one GEMM pass over dy (bf16 dy, x;
@@ -131,6 +138,11 @@ int64_t sm_attn_bwd_workspace_bytes(int dtype, int N, int L, int H, int D);
 int sm_attn_bwd(int dtype, int N, int L, int H, int D, const void* qkv, const void* o,
                 const void* dout, const float* lse, float* delta_ws, void* dqkv,
                 float scale, float drop_p, uint64_t seed, hipStream_t st);
+/* MFMA shape of the bf16 attention backward (A/B and tests; the default is the measured best):
+ * key 0 = head dim 64, key 1 = head dim 32; value 32 (v_mfma_f32_32x32x16_bf16) or 16
+ * (v_mfma_f32_16x16x32_bf16).  *prev <- the current shape; set > 0 stores value, set < 0
+ * restores the default.  Returns 0, or -2 for an unknown key / shape.  Host-side only. */
+int sm_attn_tuning(int key, int set, int value, int* prev);
 
 /* ---- LayerNorm (tiny_vit.py:112,115; decoder norm1/norm2; mae_vit_adapter.py:50) */
 int sm_layernorm_fwd(int x_dtype, int y_dtype, int64_t M, int C, const void* x, const float* gamma,
@@ -371,6 +383,13 @@ int sm_fedavg_counters_max(int num_clients, const int64_t* const* client_counter
  * (mae_loader.py:35-43).  mean3 / std3 are HOST arrays of 3 floats. */
 int sm_frames_normalize(const uint8_t* frames, const uint8_t* valid, int B, int T, int H, int W, const float* mean3,
                         const float* std3, int bgr_swap, float* out, hipStream_t st);
+
+/* ---- box calibration (bench.py; csrc/calib.hip): `blocks` workgroups of 4 waves, each wave
+ * `iters` x 8 v_mfma_f32_32x32x16_bf16 (shape 32) or the same FLOPs as 16
+ * v_mfma_f32_16x16x32_bf16 (shape 16) on random register operands.  stamps [blocks][2] int64:
+ * wave 0's s_memtime / s_memrealtime deltas (clock = d_mem / d_real x 100 MHz); sink
+ * [blocks * 256] fp32 receives the accumulators.  Returns 0 or -2 (unknown shape). */
+int sm_calibrate_mfma(int shape, int iters, int blocks, int64_t* stamps, float* sink, hipStream_t st);
 
 #ifdef __cplusplus
 }

@@ -41,9 +41,20 @@ def attn(args):
         o, lse = K.attn_fwd(qkv, N, L, H, D, p, 7)
         f = 4.0 * N * H * L * L * D
         t_f = timeit(lambda: K.attn_fwd(qkv, N, L, H, D, p, 7), args.iters)
-        t_b = timeit(lambda: K.attn_bwd(qkv, o, do, lse, N, L, H, D, p, 7), args.iters)
-        print(f"{name}: N={N} H={H} L={L} D={D} p={p}  fwd {t_f:8.2f} ms {f / t_f / 1e9:7.1f} TF/s | "
-              f"bwd {t_b:8.2f} ms {3.5 * f / t_b / 1e9:7.1f} TF/s (14 products counted)", flush=True)
+        shapes = [int(v) for v in args.bwd_shapes.split(",")] if args.bwd_shapes else [None]
+        times = {sh: [] for sh in shapes}
+        for _ in range(args.rounds):            # interleaved rounds, one process (guide rule 24)
+            for sh in shapes:
+                prev = K.attn_tuning(D, sh) if sh else None
+                times[sh].append(timeit(lambda: K.attn_bwd(qkv, o, do, lse, N, L, H, D, p, 7), args.iters))
+                if sh:
+                    K.attn_tuning(D, prev)
+        for sh in shapes:
+            ts = sorted(times[sh])
+            t_b = ts[len(ts) // 2]
+            print(f"{name}: N={N} H={H} L={L} D={D} p={p}  fwd {t_f:8.2f} ms {f / t_f / 1e9:7.1f} TF/s | "
+                  f"bwd[{sh or 'default'}] median {t_b:8.2f} ms min {ts[0]:8.2f} ms {2 * f / t_b / 1e9:7.1f} TF/s "
+                  f"(algorithmic 8BHL^2D)", flush=True)
         del qkv, do, o, lse
         torch.cuda.empty_cache()
 
@@ -302,6 +313,8 @@ if __name__ == "__main__":
     ap.add_argument("--drop", type=float, default=0.1)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--only", default="")
+    ap.add_argument("--bwd-shapes", default="", help="attn: MFMA shapes of the backward to A/B, e.g. 32,16")
+    ap.add_argument("--rounds", type=int, default=1, help="attn: interleaved rounds per backward shape")
     a = ap.parse_args()
     from ssl_mae_amd.build import build
     build()

@@ -20,7 +20,17 @@
 // Requests from any other stream get their own hipMalloc and are returned with
 // hipFree (which synchronises the device), so a block released on the home
 // stream never reaches another stream while home-stream work on it is queued.
+// Unsupported: using a home-stream block on ANOTHER stream and then releasing it while
+// that stream's work on it is still queued.  PyTorch's record_stream is a no-op under a
+// pluggable allocator, so such a block would be handed out again at once.  The training
+// step only shares persistent buffers across streams (the flat gradient buffer the
+// side-stream all-reduce reads, ssl_mae_amd/dist.py), never a temporary.
 // No graph-capture pools; statistics through sm_arena_stats.
+//
+// Running out of memory: PyTorch's pluggable-allocator hook cannot raise, so a request
+// that neither the heap nor hipMalloc can serve stops the process with the sizes.
+// Explicit memory policies are validated before the step instead
+// (tiny_vit.check_memory_policy raises a RuntimeError naming both sizes).
 #include <hip/hip_runtime_api.h>
 
 #include <cstdint>
@@ -200,6 +210,10 @@ void sm_arena_free(void* ptr, ssize_t size, int device, hipStream_t stream) {
 // statistics: out[0..7] = capacity, in use, peak in use, requests, requests served
 // by hipMalloc, free blocks, largest free block, bytes held outside the arena
 void sm_arena_stats(int device, uint64_t* out) {
+  if (device < 0 || device >= kMaxDevices) {
+    for (int i = 0; i < 8; ++i) out[i] = 0;
+    return;
+  }
   std::lock_guard<std::mutex> lk(g_mu);
   const Arena& a = g_arena[device];
   size_t fb = 0, largest = 0, foreign = 0;
@@ -214,6 +228,7 @@ void sm_arena_stats(int device, uint64_t* out) {
 }
 
 void sm_arena_reset_peak(int device) {
+  if (device < 0 || device >= kMaxDevices) return;
   std::lock_guard<std::mutex> lk(g_mu);
   g_arena[device].peak = g_arena[device].in_use;
 }

@@ -125,6 +125,11 @@ SM_DEV uint32_t attn_keep_hash(uint32_t s32, uint64_t row, uint32_t col) {
   return mix24(s32 + (uint32_t)row * AG + (col >> 2) * AC);
 }
 SM_DEV uint32_t attn_thr(float p) { return (uint32_t)(p * 128.f + 0.5f); }
+// keep-value scale 128 / (128 - thr): the inverse of the quantised keep rate (E[mask * scale] = 1)
+SM_DEV float attn_drop_scale(float p) {
+  const uint32_t t = attn_thr(p);
+  return t >= 128u ? 0.f : 128.f / (float)(128u - t);
+}
 SM_DEV bool attn_keep_byte(uint32_t h, int j, uint32_t thr) { return ((h >> (8 * j)) & 0x7Fu) >= thr; }
 
 // Packed form for bf16 P pairs: bit 7 of byte j of keep_flags() is keep(j) (7-bit
@@ -172,7 +177,7 @@ SM_DEV uint4 wide_pair(const float (&va)[4], const float (&vb)[4]) {
 SM_DEV float drop_keep_scale(const AttnArgs& a, int n, int hd, int q, int k) {
   const uint64_t row = (uint64_t)(n * a.H + hd) * a.L + q;
   const uint32_t h = attn_keep_hash(seed32(a.seed), row, (uint32_t)k);
-  return attn_keep_byte(h, k & 3, attn_thr(a.drop_p)) ? 1.0f / (1.0f - a.drop_p) : 0.0f;
+  return attn_keep_byte(h, k & 3, attn_thr(a.drop_p)) ? attn_drop_scale(a.drop_p) : 0.0f;
 }
 
 // 4x4 byte transpose inside a DPP quad: lane i's byte j <- lane j's byte i.  Stage 1
@@ -423,7 +428,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(AttnArgs a) {
   __syncthreads();
   if (lbad) pass(std::true_type{});   // block-uniform: the rerun's barriers are safe
   {
-    const float inv = (DROP ? 1.f / (1.f - a.drop_p) : 1.f) / lsum;
+    const float inv = (DROP ? attn_drop_scale(a.drop_p) : 1.f) / lsum;
     __bf16* ob = (__bf16*)a.out + ((int64_t)n * a.L + q) * C + hd * D;
 #pragma unroll
     for (int t = 0; t < D / 32; ++t)
@@ -468,7 +473,7 @@ __global__ void attn_delta_kernel(AttnArgs a, int D) {
 // as  S,dP(0)  S,dP(1) | softmax(0) | dV,dK(0) | softmax(1) | dV,dK(1)  so each
 // half's exp / dropout / dS VALU stream has the other half's MFMAs to hide under.
 // Row constants folded in: without dropout the dP accumulator starts at -Delta
-// (dS = P * acc); with it, log2(1/(1-p)) is folded into the LSE so the exp yields
+// (dS = P * acc); with it, log2 of the keep scale is folded into the LSE so the exp yields
 // P' = P/(1-p) directly (dV needs no final scale) and Delta is stored as Delta(1-p).
 template <int D, bool DROP, int NW = 4>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_bf16(AttnArgs a) {
@@ -523,8 +528,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_bf16(AttnArgs a
   for (int t = 0; t < D / 32; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) { dk[t][r] = 0.f; dv[t][r] = 0.f; }
-  const float lkeep = DROP ? log2f(1.f - a.drop_p) : 0.f;   // log2 of 1/ks
-  const float dkeep = DROP ? 1.f - a.drop_p : -1.f;         // stored Delta factor
+  const float lkeep = DROP ? -log2f(attn_drop_scale(a.drop_p)) : 0.f;   // log2 of 1/ks
+  const float dkeep = DROP ? (attn_drop_scale(a.drop_p) > 0.f ? 1.f / attn_drop_scale(a.drop_p) : 0.f) : -1.f;   // Delta factor
   const uint32_t dthr = attn_thr(a.drop_p);
   const int kq = l & 3;
   const uint32_t dlb = seed32(a.seed) + ((uint32_t)((uint64_t)(n * a.H + hd) * a.L) + 4 * h + kq) * AG +
@@ -555,7 +560,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_bf16(AttnArgs a
       da = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_b128(ldo, roff[s] + u * RB), vf[s], da, 0, 0, 0);
     }
   };
-  // P (dropped, x 1/(1-p)) and dS as bf16 B-operand fragments
+  // P (dropped, x the keep scale) and dS as bf16 B-operand fragments
   auto softmax = [&](int q0, int u, const f32x16& sa, const f32x16& da, bf16x8 (&pf)[2], bf16x8 (&sf)[2]) {
     f32x16 pv, dsv;
 #pragma unroll
@@ -724,7 +729,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_bf16(AttnArgs a) 
   for (int t = 0; t < D / 32; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) dq[t][r] = 0.f;
-  const float ks = DROP ? 1.f / (1.f - a.drop_p) : 1.f;
+  const float ks = DROP ? attn_drop_scale(a.drop_p) : 1.f;
   const uint32_t dlb = seed32(a.seed) + (uint32_t)((uint64_t)(n * a.H + hd) * a.L + q) * AG + (uint32_t)h * AC;
   const uint32_t dthr = attn_thr(a.drop_p);
 
@@ -801,6 +806,405 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_bf16(AttnArgs a) 
         const uint4 w16 = wide_pair(va, vb);
         if (qok) *(uint4*)(out + 32 * t + 8 * g + 8 * h) = w16;
       }
+  }
+}
+
+// =============================================================== bf16 backward on 16x16x32
+// The same two kernels (dK/dV with keys on lanes, dQ with queries on lanes) on
+// v_mfma_f32_16x16x32_bf16 instead of 32x32x16: equal MFMA cycles per FLOP, equal LDS
+// bytes and registers per wave, but the chip holds a higher clock on this shape
+// (MI355X_MICROARCH.md 'DVFS give-back' item 7: 1.12-1.15x the FLOP/s of the 32x32x16
+// loop on random data), and each product is a quarter of the size, so the softmax / dS
+// VALU of one 16x16 score block can start while the others are still in the matrix core.
+//
+// Fragment maps (lane l, c = l & 15, g = l >> 4): A[row c][k = 8g + j], B[k = 8g + j][col c],
+// D[row 4g + i][col c].  A wave owns 32 keys (dK/dV) or 32 queries (dQ) as two 16-column
+// groups.  A 16x16 accumulator feeds the next product as its B operand over its ROW index,
+// two blocks per 32-deep k-step: element j < 4 is row 4g + j of the first block, j >= 4 row
+// 4g + j - 4 of the second (16 rows further); the A operand of that product reads the same
+// k order with two ds_read_b64_tr_b16 (rows 4g.. and 16 + 4g..).
+template <int D>
+SM_DEV int row16_off(int ks) {   // A fragment: 8 consecutive d at k-step ks of row c
+  const int l = threadIdx.x & 63;
+  return tile_off<D>(l & 15, 32 * ks + 8 * (l >> 4));
+}
+template <int D>
+SM_DEV int tr16_off(int dt) {    // transposed A fragment (first block): rows 4g + (c>>2), cols 16 dt + 4 (c&3)
+  const int l = threadIdx.x & 63, c = l & 15;
+  return tile_off<D>(4 * (l >> 4) + (c >> 2), 16 * dt + 4 * (c & 3));
+}
+SM_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+SM_DEV bf16x8 pack_frag16(const f32x4& lo, const f32x4& hi) {
+  return __builtin_bit_cast(bf16x8, make_uint4(pack_bf16x2(lo[0], lo[1]), pack_bf16x2(lo[2], lo[3]),
+                                               pack_bf16x2(hi[0], hi[1]), pack_bf16x2(hi[2], hi[3])));
+}
+SM_DEV uint2 pack4(float a, float b, float c, float d) { return make_uint2(pack_bf16x2(a, b), pack_bf16x2(c, d)); }
+
+// dK, dV: keys on lanes (key = kbase + 16 kg + c), Q / dO tiles of 64 rows in LDS, per
+// 32-row half u: S, dP for the 2 x 2 (query group, key group) blocks, then P / dS packed
+// as B fragments per key group and dV^T / dK^T += dO^T P, Qc^T dS over 16-wide d tiles.
+// Row constants, dropout (quad byte transpose: the four keys of a hash are the four lanes
+// of a DPP quad) and the pipelined order are the 32x32x16 kernel's.
+template <int D, bool DROP, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv16_bf16(AttnArgs a) {
+  constexpr int QT = 64;
+  constexpr int RB = 16 * D * 2;   // bytes of 16 tile rows
+  constexpr int KB = 32 * NW;      // keys per block
+  constexpr int KS = D / 32, DT = D / 16;
+  __shared__ __attribute__((aligned(16))) char lq[QT * D * 2];
+  __shared__ __attribute__((aligned(16))) char ldo[QT * D * 2];
+  __shared__ __attribute__((aligned(16))) float llse[QT];
+  __shared__ __attribute__((aligned(16))) float ldel[QT];
+  const AttnTile tl((a.L + KB - 1) / KB, a.H);
+  const int n = tl.n, hd = tl.hd;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, c = l & 15, g = l >> 4;
+  const int C = a.H * D;
+  const int ldq = 3 * C;
+  const __bf16* qkv = (const __bf16*)a.qkv + (int64_t)n * a.L * ldq;
+  const __bf16* qb = a.qc + (int64_t)n * a.L * C + hd * D;
+  const __bf16* kb = qkv + C + hd * D;
+  const __bf16* vb = qkv + 2 * C + hd * D;
+  const __bf16* dob = (const __bf16*)a.dout + (int64_t)n * a.L * C + hd * D;
+  const float* lse = a.lse + ((int64_t)n * a.H + hd) * a.L;
+  const float* del = a.delta + ((int64_t)n * a.H + hd) * a.L;
+  const int kbase = tl.qb * KB + w * 32;
+  const bool wact = kbase < a.L;
+
+  bf16x8 kf[2][KS], vf[2][KS];
+#pragma unroll
+  for (int kg = 0; kg < 2; ++kg) {
+    const int key = kbase + 16 * kg + c;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (key < a.L) {
+        kf[kg][ks] = *(const bf16x8*)(kb + (int64_t)key * ldq + 32 * ks + 8 * g);
+        vf[kg][ks] = *(const bf16x8*)(vb + (int64_t)key * ldq + 32 * ks + 8 * g);
+      } else {
+        for (int j = 0; j < 8; ++j) { kf[kg][ks][j] = (__bf16)0.f; vf[kg][ks][j] = (__bf16)0.f; }
+      }
+    }
+  }
+  Stager<D, QT, 64 * NW> sq, sd;
+  sq.init(C);
+  sd.init(C);
+  int roff[KS], toff[DT];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) roff[ks] = row16_off<D>(ks);
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) toff[dt] = tr16_off<D>(dt);
+
+  f32x4 dk[2][DT], dv[2][DT];
+#pragma unroll
+  for (int kg = 0; kg < 2; ++kg)
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { dk[kg][dt][i] = 0.f; dv[kg][dt][i] = 0.f; }
+  const float ksc = DROP ? attn_drop_scale(a.drop_p) : 1.f;
+  const float lkeep = DROP ? -log2f(ksc) : 0.f;
+  const float dkeep = DROP ? (ksc > 0.f ? 1.f / ksc : 0.f) : -1.f;
+  const uint32_t dthr = attn_thr(a.drop_p);
+  const int kq = l & 3;
+  // hash input of row q0 + 32u + 16qg + 4g + kq, key group (kbase + 16kg + c) >> 2 (+ 4 kg, scalar)
+  const uint32_t dlb = seed32(a.seed) + ((uint32_t)((uint64_t)(n * a.H + hd) * a.L) + 4 * g + kq) * AG +
+                       (uint32_t)((kbase + c) >> 2) * AC;
+  uint32_t sel1, sel2;
+  quad_sel(kq, sel1, sel2);
+
+  auto sdp = [&](int u, f32x4 (&sa)[2][2], f32x4 (&da)[2][2]) {
+#pragma unroll
+    for (int qg = 0; qg < 2; ++qg) {
+      const float4 a4 = *(const float4*)&llse[32 * u + 16 * qg + 4 * g];   // -LSE2 of rows 4g + i
+      float4 b4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (!DROP) b4 = *(const float4*)&ldel[32 * u + 16 * qg + 4 * g];     // -Delta
+#pragma unroll
+      for (int kg = 0; kg < 2; ++kg) {
+        sa[qg][kg][0] = a4.x; sa[qg][kg][1] = a4.y; sa[qg][kg][2] = a4.z; sa[qg][kg][3] = a4.w;
+        da[qg][kg][0] = b4.x; da[qg][kg][1] = b4.y; da[qg][kg][2] = b4.z; da[qg][kg][3] = b4.w;
+      }
+    }
+#pragma unroll
+    for (int qg = 0; qg < 2; ++qg)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8 aq = lds_b128(lq, roff[ks] + (2 * u + qg) * RB);
+        const bf16x8 ad = lds_b128(ldo, roff[ks] + (2 * u + qg) * RB);
+#pragma unroll
+        for (int kg = 0; kg < 2; ++kg) {
+          sa[qg][kg] = mfma16(aq, kf[kg][ks], sa[qg][kg]);
+          da[qg][kg] = mfma16(ad, vf[kg][ks], da[qg][kg]);
+        }
+      }
+  };
+  auto softmax = [&](int q0, int u, const f32x4 (&sa)[2][2], const f32x4 (&da)[2][2], bf16x8 (&pf)[2],
+                     bf16x8 (&sf)[2]) {
+    f32x4 pv[2][2], dsv[2][2];
+#pragma unroll
+    for (int qg = 0; qg < 2; ++qg) {
+      float del4[4] = {0.f, 0.f, 0.f, 0.f};
+      if (DROP) {
+        const float4 b4 = *(const float4*)&ldel[32 * u + 16 * qg + 4 * g];
+        del4[0] = b4.x; del4[1] = b4.y; del4[2] = b4.z; del4[3] = b4.w;
+      }
+#pragma unroll
+      for (int kg = 0; kg < 2; ++kg) {
+        uint32_t kb4 = 0;
+        if (DROP)
+          kb4 = keep_bytes(keep_flags(
+              quad_transpose_bytes(mix24(dlb + (uint32_t)(q0 + 32 * u + 16 * qg) * AG + (uint32_t)(4 * kg) * AC),
+                                   sel1, sel2), dthr));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = __builtin_amdgcn_exp2f(sa[qg][kg][i]);
+          if (DROP) {
+            const float pk = keep_sel(p, kb4, i);
+            pv[qg][kg][i] = pk;
+            dsv[qg][kg][i] = fmaf(pk, da[qg][kg][i], -(p * del4[i]));
+          } else {
+            pv[qg][kg][i] = p;
+            dsv[qg][kg][i] = p * da[qg][kg][i];
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int kg = 0; kg < 2; ++kg) {
+      pf[kg] = pack_frag16(pv[0][kg], pv[1][kg]);
+      sf[kg] = pack_frag16(dsv[0][kg], dsv[1][kg]);
+    }
+  };
+  auto dvdk = [&](int u, const bf16x8 (&pf)[2], const bf16x8 (&sf)[2]) {
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const int o = toff[dt] + 2 * u * RB;
+      const bf16x8 ado = lds_tr(ldo, o, o + RB);
+      const bf16x8 aq = lds_tr(lq, o, o + RB);
+#pragma unroll
+      for (int kg = 0; kg < 2; ++kg) {
+        dv[kg][dt] = mfma16(ado, pf[kg], dv[kg][dt]);
+        dk[kg][dt] = mfma16(aq, sf[kg], dk[kg][dt]);
+      }
+    }
+  };
+
+  uint4 rq[Stager<D, QT, 64 * NW>::CH], rd[Stager<D, QT, 64 * NW>::CH];
+  float rlse = 0.f, rdel = 0.f;
+  auto rowc_load = [&](int q0) {
+    if (threadIdx.x < QT) {
+      const int qq = min(q0 + (int)threadIdx.x, a.L - 1);
+      rlse = lse[qq];
+      rdel = del[qq];
+    }
+  };
+  sq.load(qb, a.L, rq);
+  sd.load(dob, a.L, rd);
+  rowc_load(0);
+  for (int q0 = 0; q0 < a.L; q0 += QT) {
+    __syncthreads();
+    sq.store(lq, rq);
+    sd.store(ldo, rd);
+    if (threadIdx.x < QT) {
+      const bool ok = q0 + (int)threadIdx.x < a.L;
+      llse[threadIdx.x] = ok ? -fmaf(rlse, LOG2E, lkeep) : -1e30f;
+      ldel[threadIdx.x] = ok ? rdel * dkeep : 0.f;
+    }
+    __syncthreads();
+    if (q0 + QT < a.L) {
+      sq.load(qb + (int64_t)(q0 + QT) * C, a.L - q0 - QT, rq);
+      sd.load(dob + (int64_t)(q0 + QT) * C, a.L - q0 - QT, rd);
+      rowc_load(q0 + QT);
+    }
+    if (!wact) continue;
+    f32x4 s0[2][2], p0[2][2], s1[2][2], p1[2][2];
+    bf16x8 pf0[2], sf0[2], pf1[2], sf1[2];
+    sdp(0, s0, p0);
+    sdp(1, s1, p1);
+    softmax(q0, 0, s0, p0, pf0, sf0);
+    dvdk(0, pf0, sf0);
+    softmax(q0, 1, s1, p1, pf1, sf1);
+    dvdk(1, pf1, sf1);
+  }
+  // lane: dK / dV [key kbase + 16 kg + c][16 dt + 4g + i]: 8-B runs
+#pragma unroll
+  for (int kg = 0; kg < 2; ++kg) {
+    const int key = kbase + 16 * kg + c;
+    if (key >= a.L) continue;
+    __bf16* out = (__bf16*)a.out + ((int64_t)n * a.L + key) * ldq + hd * D + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      *(uint2*)(out + C + 16 * dt) = pack4(dk[kg][dt][0] * LN2, dk[kg][dt][1] * LN2, dk[kg][dt][2] * LN2,
+                                           dk[kg][dt][3] * LN2);
+      *(uint2*)(out + 2 * C + 16 * dt) = pack4(dv[kg][dt][0], dv[kg][dt][1], dv[kg][dt][2], dv[kg][dt][3]);
+    }
+  }
+}
+
+// dQ: queries on lanes (q = qbase + 16 qg + c), K / V tiles of 64 keys in LDS; per 32-key
+// half s the 2 x 2 (key group, query group) blocks of S^T, dP^T, then dS^T packed per
+// query group and dQ^T += K^T dS^T over 16-wide d tiles.  The prologue forms Delta and
+// writes bf16(Q scale log2 e) for the dK/dV kernel, as the 32x32x16 kernel.
+template <int D, bool DROP, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq16_bf16(AttnArgs a) {
+  constexpr int KT = 64;
+  constexpr int RB = 16 * D * 2;
+  constexpr int QB = 32 * NW;
+  constexpr int KS = D / 32, DT = D / 16;
+  __shared__ __attribute__((aligned(16))) char lk[KT * D * 2];
+  __shared__ __attribute__((aligned(16))) char lv[KT * D * 2];
+  const AttnTile tl((a.L + QB - 1) / QB, a.H);
+  const int n = tl.n, hd = tl.hd;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, c = l & 15, g = l >> 4;
+  const int C = a.H * D;
+  const int ldq = 3 * C;
+  const __bf16* qkv = (const __bf16*)a.qkv + (int64_t)n * a.L * ldq;
+  const __bf16* qb = qkv + hd * D;
+  const __bf16* kb = qkv + C + hd * D;
+  const __bf16* vb = qkv + 2 * C + hd * D;
+  const __bf16* dob = (const __bf16*)a.dout + (int64_t)n * a.L * C + hd * D;
+  const __bf16* ob = (const __bf16*)a.o + (int64_t)n * a.L * C + hd * D;
+  const int qbase = tl.qb * QB + w * 32;
+  const bool wact = qbase < a.L;
+
+  bf16x8 qf[2][KS], df[2][KS];
+  float lse2[2], dl[2];
+#pragma unroll
+  for (int qg = 0; qg < 2; ++qg) {
+    const int q = qbase + 16 * qg + c;
+    const bool qok = q < a.L;
+    lse2[qg] = qok ? a.lse[((int64_t)n * a.H + hd) * a.L + q] * LOG2E : 1e30f;
+    float dpart = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (qok) {
+        qf[qg][ks] = *(const bf16x8*)(qb + (int64_t)q * ldq + 32 * ks + 8 * g);
+        df[qg][ks] = *(const bf16x8*)(dob + (int64_t)q * C + 32 * ks + 8 * g);
+        const bf16x8 of = *(const bf16x8*)(ob + (int64_t)q * C + 32 * ks + 8 * g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dpart = fmaf((float)df[qg][ks][j], (float)of[j], dpart);
+      } else {
+        for (int j = 0; j < 8; ++j) { qf[qg][ks][j] = (__bf16)0.f; df[qg][ks][j] = (__bf16)0.f; }
+      }
+    }
+    // the row's four d groups live in lanes c, c + 16, c + 32, c + 48
+    dpart += __shfl_xor(dpart, 16);
+    dpart += __shfl_xor(dpart, 32);
+    dl[qg] = dpart;
+    if (qok && g == 0) a.delta[((int64_t)n * a.H + hd) * a.L + q] = dpart;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[qg][ks][j] = (__bf16)((float)qf[qg][ks][j] * (a.scale * LOG2E));
+      if (qok) *(bf16x8*)(a.qc + ((int64_t)n * a.L + q) * C + hd * D + 32 * ks + 8 * g) = qf[qg][ks];
+    }
+  }
+  Stager<D, KT, 64 * NW> stg;
+  stg.init(ldq);
+  int roff[KS], toff[DT];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) roff[ks] = row16_off<D>(ks);
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) toff[dt] = tr16_off<D>(dt);
+  f32x4 dq[2][DT];
+#pragma unroll
+  for (int qg = 0; qg < 2; ++qg)
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dq[qg][dt][i] = 0.f;
+  const float ksc = DROP ? attn_drop_scale(a.drop_p) : 1.f;
+  const uint32_t dthr = attn_thr(a.drop_p);
+  uint32_t dlb[2];   // hash input of this lane's row, key group (k0 + 32 s + 16 kk + 4 g) >> 2 minus its scalar part
+#pragma unroll
+  for (int qg = 0; qg < 2; ++qg)
+    dlb[qg] = seed32(a.seed) + (uint32_t)((uint64_t)(n * a.H + hd) * a.L + qbase + 16 * qg + c) * AG +
+              (uint32_t)g * AC;
+
+  uint4 rk[Stager<D, KT, 64 * NW>::CH], rv[Stager<D, KT, 64 * NW>::CH];
+  stg.load(kb, a.L, rk);
+  stg.load(vb, a.L, rv);
+  auto tile = [&](int k0, auto rag) {
+    constexpr bool RAGGED = decltype(rag)::value;
+    __syncthreads();
+    stg.store(lk, rk);
+    stg.store(lv, rv);
+    __syncthreads();
+    if (k0 + KT < a.L) {
+      stg.load(kb + (int64_t)(k0 + KT) * ldq, a.L - k0 - KT, rk);
+      stg.load(vb + (int64_t)(k0 + KT) * ldq, a.L - k0 - KT, rv);
+    }
+    if (!wact) return;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (RAGGED && s == 1 && k0 + 32 >= a.L) continue;   // no key below L in this half
+      f32x4 sacc[2][2], dpacc[2][2];   // [key group kk][query group]
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int qg = 0; qg < 2; ++qg)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) { sacc[kk][qg][i] = -lse2[qg]; dpacc[kk][qg][i] = 0.f; }
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const bf16x8 ak = lds_b128(lk, roff[ks] + (2 * s + kk) * RB);
+          const bf16x8 av = lds_b128(lv, roff[ks] + (2 * s + kk) * RB);
+#pragma unroll
+          for (int qg = 0; qg < 2; ++qg) {
+            sacc[kk][qg] = mfma16(ak, qf[qg][ks], sacc[kk][qg]);
+            dpacc[kk][qg] = mfma16(av, df[qg][ks], dpacc[kk][qg]);
+          }
+        }
+      if constexpr (RAGGED) {   // keys past L: P = exp2(-huge) = 0 (last tile only)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int qg = 0; qg < 2; ++qg)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              if (k0 + 32 * s + 16 * kk + 4 * g + i >= a.L) sacc[kk][qg][i] = NEG_BIG;
+      }
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int qg = 0; qg < 2; ++qg) {
+          uint32_t hv = 0;
+          if (DROP) hv = keep_bytes(keep_flags(mix24(dlb[qg] + (uint32_t)((k0 >> 2) + 8 * s + 4 * kk) * AC), dthr));
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float p = __builtin_amdgcn_exp2f(sacc[kk][qg][i]);
+            const float dp = dpacc[kk][qg][i];
+            if (DROP) dpacc[kk][qg][i] = p * fmaf(keep_sel(dp, hv, i), ksc, -dl[qg]);
+            else dpacc[kk][qg][i] = p * (dp - dl[qg]);
+          }
+        }
+      bf16x8 sf[2];
+#pragma unroll
+      for (int qg = 0; qg < 2; ++qg) sf[qg] = pack_frag16(dpacc[0][qg], dpacc[1][qg]);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const int o = toff[dt] + 2 * s * RB;
+        const bf16x8 ak = lds_tr(lk, o, o + RB);
+#pragma unroll
+        for (int qg = 0; qg < 2; ++qg) dq[qg][dt] = mfma16(ak, sf[qg], dq[qg][dt]);
+      }
+    }
+  };
+  int k0 = 0;
+  for (; k0 + KT <= a.L; k0 += KT) tile(k0, std::false_type{});
+  if (k0 < a.L) tile(k0, std::true_type{});
+  // lane: dQ [q][16 dt + 4g + i]: 8-B runs
+#pragma unroll
+  for (int qg = 0; qg < 2; ++qg) {
+    const int q = qbase + 16 * qg + c;
+    if (q >= a.L) continue;
+    __bf16* out = (__bf16*)a.out + ((int64_t)n * a.L + q) * ldq + hd * D + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+      *(uint2*)(out + 16 * dt) = pack4(dq[qg][dt][0] * a.scale, dq[qg][dt][1] * a.scale, dq[qg][dt][2] * a.scale,
+                                       dq[qg][dt][3] * a.scale);
   }
 }
 
@@ -942,9 +1346,17 @@ __global__ __launch_bounds__(128) void attn_bwd_dkdv_f32(AttnArgs a) {
 // dQ first: it forms Delta = rowsum(dO*O) in its prologue and writes bf16(Q scale log2 e)
 // for the dK/dV kernel.  (8-wave blocks and a static s_setprio for one wave of each SIMD
 // pair measured 1-10 % slower, profiles/r04c_attn_bwd_variants.txt.)
+// MFMA shape of the bf16 backward per head dim (sm_attn_tuning: 32 = v_mfma_f32_32x32x16_bf16,
+// 16 = v_mfma_f32_16x16x32_bf16); key 0: D = 64 (decoder), key 1: D = 32 (encoder).
+int g_attn_bwd_shape[2] = {32, 32};
 template <int D, bool DROP>
 void launch_attn_bwd(const AttnArgs& a, hipStream_t st) {
   const dim3 g4((unsigned)((a.L + 127) / 128) * (unsigned)(a.H * a.N));
+  if (g_attn_bwd_shape[D == 64 ? 0 : 1] == 16) {
+    hipLaunchKernelGGL((attn_bwd_dq16_bf16<D, DROP>), g4, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((attn_bwd_dkdv16_bf16<D, DROP>), g4, dim3(256), 0, st, a);
+    return;
+  }
   hipLaunchKernelGGL((attn_bwd_dq_bf16<D, DROP>), g4, dim3(256), 0, st, a);
   hipLaunchKernelGGL((attn_bwd_dkdv_bf16<D, DROP>), g4, dim3(256), 0, st, a);
 }
@@ -1012,5 +1424,19 @@ extern "C" int sm_attn_bwd(int dtype, int N, int L, int H, int D, const void* qk
     }
   }
   SM_CHECK_LAUNCH();
+  return 0;
+}
+
+// A/B switch of the bf16 backward's MFMA shape (see launch_attn_bwd): key 0 = D 64, 1 = D 32;
+// *prev <- current shape; set > 0 stores value (16 or 32), set < 0 restores 32.  Host-side only.
+extern "C" int sm_attn_tuning(int key, int set, int value, int* prev) {
+  if (key < 0 || key > 1) return -2;
+  if (prev) *prev = g_attn_bwd_shape[key];
+  if (set > 0) {
+    if (value != 16 && value != 32) return -2;
+    g_attn_bwd_shape[key] = value;
+  } else if (set < 0) {
+    g_attn_bwd_shape[key] = 32;
+  }
   return 0;
 }

@@ -236,7 +236,7 @@ SM_DEV float block_sum(float v, float* red) {
 // Dropout / DropPath masks are a pure function of (seed, row, column):
 //   h    = fmix32(seed32 + row * 0x9E3779B1 + (col >> 2) * 0x7FEB352D)
 //   byte = (h >> 8 * (col & 3)) & 0xFF                 (one hash per 4 columns)
-//   keep = byte >= round(256 p)                        (kept values scaled by 1/(1-p))
+//   keep = byte >= round(256 p)                        (kept values scaled by 256/(256-thr))
 // Every kernel that touches an element (forward, checkpoint recompute, backward)
 // regenerates the same mask without storing it.  `row` is the tensor row (or the
 // attention row (n*H + h)*L + q); fmix32 is MurmurHash3's finalizer.  The 8-bit
@@ -254,6 +254,13 @@ SM_DEV uint32_t seed32(uint64_t seed) { return (uint32_t)seed ^ (uint32_t)(seed 
 SM_DEV uint32_t drop_rowbase(uint32_t s32, uint64_t row) { return s32 + (uint32_t)row * 0x9E3779B1u; }
 SM_DEV uint32_t drop_hash(uint32_t rowbase, uint32_t col) { return fmix32(rowbase + (col >> 2) * 0x7FEB352Du); }
 SM_DEV uint32_t drop_thr(float p) { return (uint32_t)(p * 256.f + 0.5f); }
+// Kept values are scaled by 256 / (256 - thr), the inverse of the quantised keep rate, so
+// E[mask * scale] = 1 exactly as nn.Dropout / timm DropPath (1 / (1 - p) with the 8-bit
+// threshold would leave E = (256 - thr) / 256 / (1 - p): 0.99826 at p = 0.1).
+SM_DEV float drop_scale(float p) {
+  const uint32_t t = drop_thr(p);
+  return t >= 256u ? 0.f : 256.f / (float)(256u - t);
+}
 SM_DEV bool drop_keep_bits(uint32_t h, uint32_t col, uint32_t thr) {
   return ((h >> ((col & 3) * 8)) & 0xFFu) >= thr;
 }

@@ -83,7 +83,7 @@ SM_DEV void epilogue_store(const GemmArgs& g, int64_t row, int col, float acc, i
     v = gelu_f(v);
   }
   if (g.drop_p > 0.f)
-    v *= drop_keep(seed32(g.seed), (uint64_t)row, (uint32_t)col, drop_thr(g.drop_p)) ? 1.f / (1.f - g.drop_p) : 0.f;
+    v *= drop_keep(seed32(g.seed), (uint64_t)row, (uint32_t)col, drop_thr(g.drop_p)) ? drop_scale(g.drop_p) : 0.f;
   if (g.row_scale) v *= g.row_scale[row / g.rows_per_group];
   if (g.beta != 0.f) v += g.beta * to_f<TC>(g.R ? ((const TC*)g.R)[idx] : C[idx]);
   C[idx] = from_f<TC>(v);
@@ -325,7 +325,7 @@ SM_DEV __attribute__((always_inline)) void gemm_epilogue(const GemmArgs& g, f32x
   const bool has_r = g.beta != 0.f;
   const TC* Rsrc = g.R ? (const TC*)g.R : (const TC*)g.C;
   const uint32_t s32 = seed32(g.seed), thr = drop_thr(g.drop_p);
-  const float ks = g.drop_p > 0.f ? 1.f / (1.f - g.drop_p) : 1.f;
+  const float ks = g.drop_p > 0.f ? drop_scale(g.drop_p) : 1.f;
   constexpr int RW = sizeof(TC) * 8 / 16;   // 16-B words per 8-column run
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
@@ -808,7 +808,7 @@ struct XformColsB {
       }
     } else {
       const uint32_t thr = drop_thr(g.xb_p);
-      const float ks = g.xb_p > 0.f ? 1.f / (1.f - g.xb_p) : 1.f;
+      const float ks = g.xb_p > 0.f ? drop_scale(g.xb_p) : 1.f;
 #pragma unroll
       for (int i = 0; i < CH; ++i) {
         float x[8], v[8];
@@ -1073,7 +1073,7 @@ SM_DEV __attribute__((always_inline)) void pp_stage(const GemmArgs& g, const f32
   const bool has_r = g.beta != 0.f;
   const __bf16* Rsrc = g.R ? (const __bf16*)g.R : (const __bf16*)g.C;
   const uint32_t s32 = seed32(g.seed), thr = drop_thr(g.drop_p);
-  const float ks = g.drop_p > 0.f ? 1.f / (1.f - g.drop_p) : 1.f;
+  const float ks = g.drop_p > 0.f ? drop_scale(g.drop_p) : 1.f;
   const auto brs = __builtin_amdgcn_make_buffer_rsrc((void*)g.bias, (short)0, g.bias ? g.N * 4 : 0, 0x00020000);
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -1158,7 +1158,7 @@ SM_DEV __attribute__((always_inline)) void pp_stage_gelu_aux(const GemmArgs& g, 
                                                              int wm, int wn, int l, char* img) {
   const int h = l >> 5;
   const uint32_t s32 = seed32(g.seed), thr = drop_thr(g.drop_p);
-  const float ks = g.drop_p > 0.f ? 1.f / (1.f - g.drop_p) : 1.f;
+  const float ks = g.drop_p > 0.f ? drop_scale(g.drop_p) : 1.f;
   const auto brs = __builtin_amdgcn_make_buffer_rsrc((void*)g.bias, (short)0, g.bias ? g.N * 4 : 0, 0x00020000);
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -1583,19 +1583,21 @@ int choose_splits(int M, int N, int K, bool bf16) {
 // bf16 kernel variant: 1 = gemm_bf16_kernel (128 x 128, 4 waves), 2 = gemm_bf16_v2 at
 // BM = 256 (8 waves), 3 = gemm_bf16_v2 at BM = 128.  Default (0): v2, BM = 256 when
 // M >= 192 (a 256-row tile half empty loses to BM = 128 there: dW of the 96-channel
-// MBConv projection).  SM_GEMM_VARIANT pins one (A/B measurement runs).
+// MBConv projection).  sm_gemm_tuning(TUNE_VARIANT) pins one (A/B measurement runs).
 // Measured and dropped (round 2): a 256 x 256 tile on 8 waves of 128 x 64 (0.75 KB of
 // fragment reads and 256 B of LDS-DMA staging per MFMA instead of v2's 1 KB + 384 B),
 // double-buffered buffer -> LDS DMA, one block per CU: 20-30 % slower than v2 on every
 // weight gradient of the step (profiles/r02g/dw_wide.txt).  Its operand delivery per CU
 // (64 KB in flight, ~21 GB/s) is the bound, not the LDS; v2's two resident blocks keep
 // 96 KB in flight.
+// Tuning knobs (A/B measurement runs only; scripts/ set them through sm_gemm_tuning, the
+// product path never changes them).  Defaults are the measured best per shape family.
+enum { TUNE_VARIANT = 0, TUNE_PP = 1, TUNE_PP_MINN = 2, TUNE_PP_MAXK = 3, TUNE_PP_ROUNDS = 4,
+       TUNE_PP_ROUNDS_SMALLK = 5, TUNE_PP_ROUNDS_MIDK = 6, TUNE_COUNT = 7 };
+constexpr int kTuneDefault[TUNE_COUNT] = {0, 1, 512, 6 * BKT, -1, 8, 2};
+int g_tune[TUNE_COUNT] = {0, 1, 512, 6 * BKT, -1, 8, 2};
 int gemm_variant(int M, int N, int K) {
-  static const int forced = [] {
-    const char* e = getenv("SM_GEMM_VARIANT");
-    const int x = e ? atoi(e) : 0;
-    return (x >= 1 && x <= 3) ? x : 0;
-  }();
+  const int forced = (g_tune[TUNE_VARIANT] >= 1 && g_tune[TUNE_VARIANT] <= 3) ? g_tune[TUNE_VARIANT] : 0;
   if (forced) return forced;
   // 384-row weight gradients with narrow rows (dW [384][384], [384][96]): three full
   // 128-row tiles instead of two 256-row tiles, one a quarter empty -- measured
@@ -1610,16 +1612,9 @@ int variant_bn(int v) { return 128; (void)v; }
 
 // Persistent pipelined form (gemm_bf16_pp) for a non-split bf16 GEMM with a K-major A at
 // BM = 256 whose epilogue has no side output: used when the grid would take more than one
-// round of resident blocks.  sm_gemm_persistent(0) (or SM_GEMM_PP=0 at process start) selects
+// round of resident blocks.  sm_gemm_persistent(0) (sm_gemm_tuning(TUNE_PP)) selects
 // the one-tile-per-block v2 form; both give bit-identical outputs.
-int pp_mode = -1;   // -1: not yet read from the environment
-bool pp_enabled() {
-  if (pp_mode < 0) {
-    const char* e = getenv("SM_GEMM_PP");
-    pp_mode = (e && e[0] == '0') ? 0 : 1;
-  }
-  return pp_mode != 0;
-}
+bool pp_enabled() { return g_tune[TUNE_PP] != 0; }
 // Where it pays (same-box A/B, profiles/r05b_gemm_persistent_ab.txt, r05aa_gemm_pp_rounds.txt): K <= 128
 // (write-bound: stage-0 expand / projection data gradient -4..-13 %), and K <= 384 at N >= 512
 // (several n-tiles share each A panel: decoder qkv / fc1 forward -6..-7 %, fc2 data gradient
@@ -1627,21 +1622,15 @@ bool pp_enabled() {
 // there is no A panel to share.  Blocks take at most pp_rounds() tiles each (8 at K <= 128, 2
 // above): fully persistent blocks drift apart, so the n-tile blocks that share an A panel no
 // longer stream it through L2 together (K = 384: -1..+1 % persistent against -6 % at 2 tiles).
-int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
 bool pp_ok(const GemmArgs& g) {
-  static const int pp_minn = env_int("SM_GEMM_PP_MINN", 512), pp_maxk = env_int("SM_GEMM_PP_MAXK", 6 * BKT);   // A/B
   return pp_enabled() && g.partial == nullptr && g.colsum == nullptr && !g.ctrans && !(g.epi & 4) &&
          (!((g.epi & 1) && g.aux) || (g.beta == 0.f && g.row_scale == nullptr)) && g.aux_out == nullptr &&
          g.K > 0 && g.k_begin == 0 && g.k_chunk >= g.K &&
-         (g.K <= 2 * BKT || (g.K <= pp_maxk && g.N >= pp_minn));
+         (g.K <= 2 * BKT || (g.K <= g_tune[TUNE_PP_MAXK] && g.N >= g_tune[TUNE_PP_MINN]));
 }
 int pp_rounds(const GemmArgs& g) {
-  static const int forced = env_int("SM_GEMM_PP_ROUNDS", -1);   // A/B runs; 0 = fully persistent
-  static const int small_k = env_int("SM_GEMM_PP_ROUNDS_SMALLK", 8), mid_k = env_int("SM_GEMM_PP_ROUNDS_MIDK", 2);
-  return forced >= 0 ? forced : g.K <= 2 * BKT ? small_k : mid_k;
+  const int forced = g_tune[TUNE_PP_ROUNDS];   // A/B runs; 0 = fully persistent
+  return forced >= 0 ? forced : g.K <= 2 * BKT ? g_tune[TUNE_PP_ROUNDS_SMALLK] : g_tune[TUNE_PP_ROUNDS_MIDK];
 }
 template <bool BK, int IMP>
 bool launch_pp(const GemmArgs& g, hipStream_t st) {
@@ -1807,8 +1796,19 @@ extern "C" int sm_conv3x3_wgrad(const void* dy, const void* x, float* dw, int ac
 
 extern "C" int sm_gemm_persistent(int mode) {
   const int prev = pp_enabled() ? 1 : 0;
-  if (mode >= 0) pp_mode = mode ? 1 : 0;
+  if (mode >= 0) g_tune[TUNE_PP] = mode ? 1 : 0;
   return prev;
+}
+
+// A/B tuning knob `key` (TUNE_* above): *prev <- its current value; set != 0 stores `value`
+// (set < 0 restores the default).  Host-side only, no launch.  Returns 0, or -2 for an
+// unknown key.  Not thread-safe against concurrent GEMM launches: set before the run.
+extern "C" int sm_gemm_tuning(int key, int set, int value, int* prev) {
+  if (key < 0 || key >= TUNE_COUNT) return -2;
+  if (prev) *prev = g_tune[key];
+  if (set > 0) g_tune[key] = value;
+  else if (set < 0) g_tune[key] = kTuneDefault[key];
+  return 0;
 }
 
 extern "C" int64_t sm_gemm_workspace_bytes(int ab_dtype, int M, int N, int K) {

@@ -281,7 +281,7 @@ __global__ __launch_bounds__(256) void ln_bwd16_kernel(const TD* dy, const TI* x
       store4_nt(dx + e0 + 4 * G * u, o);
       if (br.bo) {
         const float rsv = br.rs ? br.rs[row / br.rpg] : 1.f;
-        const float ks = br.p > 0.f ? 1.f / (1.f - br.p) : 1.f;
+        const float ks = br.p > 0.f ? drop_scale(br.p) : 1.f;
         const uint32_t hsh = br.p > 0.f ? drop_hash(drop_rowbase(seed32(br.seed), (uint64_t)row),
                                                      (uint32_t)(4 * G * u + 4 * gl)) : 0u;
         const uint32_t thr = drop_thr(br.p);
@@ -585,7 +585,7 @@ __global__ __launch_bounds__(256) void bn_bwd_dx_kernel(const TD* dy, const TI* 
 // ============================================================ elementwise
 // 8 consecutive elements of one row (ncols % 8 == 0): dropout multipliers
 SM_DEV void drop_mult8(int64_t e, int ncols, float drop_p, uint64_t seed, float* m) {
-  const float ks = 1.f / (1.f - drop_p);
+  const float ks = drop_scale(drop_p);
   const int64_t row = e / ncols;
   const uint32_t c0 = (uint32_t)(e - row * ncols);
   const uint32_t rb = drop_rowbase(seed32(seed), (uint64_t)row), thr = drop_thr(drop_p);
@@ -641,7 +641,7 @@ __global__ void dropout_bwd_kernel(const T* dy, TO* dx, int64_t total8, int ncol
 
 __global__ void droppath_scale_kernel(int n, float p, uint64_t seed, float* out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = drop_keep(seed32(seed), (uint64_t)i, 0u, drop_thr(p)) ? 1.f / (1.f - p) : 0.f;
+  if (i < n) out[i] = drop_keep(seed32(seed), (uint64_t)i, 0u, drop_thr(p)) ? drop_scale(p) : 0.f;
 }
 
 template <typename TA, typename TB, typename TO>

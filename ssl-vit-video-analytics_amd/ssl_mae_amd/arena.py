@@ -40,7 +40,7 @@ def _bind(path):
 def library():
     """The arena library bound with ctypes (built in-tree if missing)."""
     if _state.get("raw") is None:
-        _state["raw"] = _bind(build_arena() if not os.path.exists(ARENA_LIB) else ARENA_LIB)
+        _state["raw"] = _bind(build_arena())   # no-op when the library is newer than csrc/arena.cpp
     return _state["raw"]
 
 
@@ -64,7 +64,10 @@ def active():
 
 def stats(device=None):
     """The arena's counters for `device` (bytes / counts, see csrc/arena.cpp)."""
-    dev = torch.cuda.current_device() if device is None else int(getattr(device, "index", device) or 0)
+    if device is None or (isinstance(device, torch.device) and device.index is None):
+        dev = torch.cuda.current_device()
+    else:
+        dev = int(getattr(device, "index", device))
     out = (ctypes.c_uint64 * 8)()
     library().sm_arena_stats(dev, out)
     return dict(zip(_FIELDS, (int(v) for v in out)))

@@ -45,6 +45,60 @@ def gemm_persistent(mode=-1):
     return int(query("sm_gemm_persistent", int(mode)))
 
 
+GEMM_TUNING_KEYS = ("variant", "pp", "pp_min_n", "pp_max_k", "pp_rounds", "pp_rounds_small_k", "pp_rounds_mid_k")
+
+
+def gemm_tuning(key, value=None, reset=False):
+    """A/B knob of the GEMM dispatch (sm_gemm_tuning; scripts/ only, the product path never
+    sets one): returns the current value of `key` (GEMM_TUNING_KEYS), then stores `value`
+    (or the default with reset=True)."""
+    import ctypes
+    k = GEMM_TUNING_KEYS.index(key)
+    prev = ctypes.c_int(0)
+    call("sm_gemm_tuning", k, -1 if reset else (1 if value is not None else 0), int(value or 0),
+         ctypes.addressof(prev))
+    return prev.value
+
+
+_GEMM_TUNING_DEFAULTS = {"variant": 0, "pp": 1, "pp_min_n": 512, "pp_max_k": 384, "pp_rounds": -1,
+                         "pp_rounds_small_k": 8, "pp_rounds_mid_k": 2}
+
+
+def gemm_tuning_nondefault():
+    """{key: value} of every GEMM knob not at its default (reported in bench.py's config)."""
+    out = {}
+    for k, d in _GEMM_TUNING_DEFAULTS.items():
+        v = gemm_tuning(k)
+        if v != d:
+            out[k] = v
+    return out
+
+
+def calibrate_mfma(shape=32, iters=20000, blocks=None, device=None):
+    """Bare bf16 MFMA loop on random register data (csrc/calib.hip), the box calibration of
+    bench.py: shape 32 = v_mfma_f32_32x32x16_bf16, 16 = v_mfma_f32_16x16x32_bf16; `blocks`
+    workgroups of 4 waves (default 2 per CU).  Returns (TFLOP/s, median in-kernel clock MHz,
+    ms) over one timed launch after a warm-up launch."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    if blocks is None:
+        blocks = 2 * torch.cuda.get_device_properties(dev).multi_processor_count
+    stamps = torch.zeros(blocks, 2, dtype=torch.int64, device=dev)
+    sink = torch.zeros(blocks * 256, dtype=torch.float32, device=dev)
+    call("sm_calibrate_mfma", int(shape), max(1, int(iters) // 10), int(blocks), ptr(stamps), ptr(sink), stream())   # warm-up
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    call("sm_calibrate_mfma", int(shape), int(iters), int(blocks), ptr(stamps), ptr(sink), stream())
+    e.record()
+    e.synchronize()
+    ms = s.elapsed_time(e)
+    flop = 2.0 * 32 * 32 * 16 * 8 * iters * 4 * blocks    # 8 MFMAs (32x32x16 or 2x 16x16x32 pairs) per iter
+    st = stamps.cpu()
+    mem, real = st[:, 0].double(), st[:, 1].double()
+    ok = real > 0
+    mhz = float((mem[ok] / real[ok] * 100.0).median()) if ok.any() else None
+    return flop / (ms * 1e-3) / 1e12, mhz, ms
+
+
 def linear(x, w, bias=None, out_dtype=None, gelu=False, residual=None, round_branch=False, drop_p=0.0, seed=0,
            row_scale=None, rows_per_group=1):
     """y = residual + rs[row] * drop(act(x @ w^T + bias)); returns (y, pre-activation) with GELU."""
@@ -218,6 +272,17 @@ def colsum(x, out, accumulate=True):
 
 
 # ------------------------------------------------------------------ attention
+def attn_tuning(D, shape=None, reset=False):
+    """MFMA shape of the bf16 attention backward for head dim D (sm_attn_tuning): 32 =
+    v_mfma_f32_32x32x16_bf16, 16 = v_mfma_f32_16x16x32_bf16.  Returns the current shape,
+    then stores `shape` (or the default with reset=True).  Tests and A/B scripts only."""
+    import ctypes
+    prev = ctypes.c_int(0)
+    call("sm_attn_tuning", 0 if D == 64 else 1, -1 if reset else (1 if shape is not None else 0), int(shape or 0),
+         ctypes.addressof(prev))
+    return prev.value
+
+
 def attn_fwd(qkv, N, L, H, D, drop_p=0.0, seed=0):
     _chk(qkv)
     out = torch.empty((N * L, H * D), dtype=qkv.dtype, device=qkv.device)

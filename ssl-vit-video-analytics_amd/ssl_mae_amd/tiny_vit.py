@@ -19,8 +19,10 @@ from .functions import BlockFn, MBConvFn, Mode, StemFn
 
 class DropPath(nn.Module):
     """Stochastic depth (timm.layers.DropPath semantics: per-sample keep with
-    probability 1-p, kept samples scaled by 1/(1-p)); applied inside the fused
-    kernels as a per-row-group scale of the residual branch."""
+    probability 1-p, E[mask * scale] = 1); applied inside the fused kernels as a
+    per-row-group scale of the residual branch.  The keep test is the counter hash's
+    8-bit threshold round(256 p), so kept samples are scaled by 256 / (256 - round(256 p)),
+    the inverse of the quantised keep rate (csrc/common.h drop_scale)."""
 
     def __init__(self, drop_prob=0.0):
         super().__init__()
@@ -243,9 +245,12 @@ class TinyViT(nn.Module):
         if resident == "auto":
             resident = auto_resident_stages(x.shape[0], x.shape[1] * 2, mode.bf16, x.device, key=key) \
                 if self.use_checkpoint and self.training and grad else ()
+        explicit = self.resident_stages != "auto" or lite != "auto"
         if lite == "auto":
             lite = auto_lite_stages(x.shape[0], x.shape[1] * 2, mode.bf16, x.device, resident, key=key) \
                 if self.use_checkpoint and self.training and grad else ()
+        if explicit and self.use_checkpoint and self.training and grad:
+            check_memory_policy(x.shape[0], x.shape[1] * 2, mode.bf16, x.device, resident, lite, key=key)
         for i in range(n_stages):
             stage = self.stages[i]
             xb = x_bn if i == 0 else None
@@ -308,6 +313,67 @@ _PEAK_GIB_PER_FRAME = {
     # (0,) (stage 0 resident, arena only) 231.2 GiB, +3.2 % (profiles/r05ap_small_stage0_resident.txt)
     ((2, 2, 12, 2), 8): {(0,): 231.2 / 2048, (): 184.0 / 2048},
 }
+
+
+# Policies measured to run out of memory at B = 256 (GiB per frame: the memory in use when the
+# failing request arrived plus that request, a LOWER bound on the policy's peak).  C3 ViT-Small
+# with stage 2 resident: 295.1 GB in use + a 4.9 GB request (profiles/r05ap_small_stage0_resident.txt).
+_PEAK_LOWER_BOUND_GIB_PER_FRAME = {((2, 2, 12, 2), 8): {(2,): (295123654656 + 4932501504) / 2 ** 30 / 2048}}
+
+
+def predicted_peak_gib(frames, image_size, bf16, resident, lite=(), key=((2, 2, 6, 2), 4)):
+    """(GiB, basis) of one training step's peak under a resident / lite policy, from the
+    measured tables: basis "measured", "lower bound" (the policy, or a subset of it, was
+    measured out of memory) or "estimate" (the all-checkpointed peak plus per-block stage
+    costs taken from the TinyViT-21M measurements); (None, None) for an unmeasured model."""
+    resident, lite = tuple(sorted(resident)), tuple(sorted(lite))
+    scale = frames * (image_size / 224.0) ** 2 * (1 if bf16 else 2)
+    table = _PEAK_GIB_PER_FRAME.get(key)
+    if table is None:
+        return None, None
+    extra = 0.0
+    if lite:
+        e = _LITE0_EXTRA_GIB_PER_FRAME.get((key, resident))
+        extra = e if e is not None else 0.0
+    if resident in table:
+        return (table[resident] + extra) * scale, "measured"
+    lb = _PEAK_LOWER_BOUND_GIB_PER_FRAME.get(key, {})
+    bounds = [v for pol, v in lb.items() if set(pol) <= set(resident)]
+    if bounds:
+        return max(bounds) * scale, "lower bound"
+    if () not in table:
+        return None, None
+    t = _PEAK_GIB_PER_FRAME[((2, 2, 6, 2), 4)]
+    per_block = {2: (t[(2,)] - t[()]) / 6, 1: (t[(1, 2)] - t[(2,)]) / 2, 0: (t[(0, 1, 2)] - t[(1, 2)]) / 2}
+    depths = key[0]
+    est = table[()] + sum(per_block[s] * depths[s] for s in resident if s in per_block)
+    return (est + extra) * scale, "estimate"
+
+
+def check_memory_policy(frames, image_size, bf16, device, resident, lite=(), key=((2, 2, 6, 2), 4),
+                        arena_budget=0.96):
+    """Raise RuntimeError before the step when an explicitly requested resident / lite policy
+    cannot fit: its predicted peak (predicted_peak_gib) against `arena_budget` of the
+    device-memory arena's capacity (the rest is fragmentation headroom: the measured C3
+    stage-2 failure met a 4.6 GiB request with 6.5 GiB free but split), or, under the caching
+    allocator, the device's total memory.  The arena would otherwise meet the failing request
+    deep inside the step, where PyTorch's pluggable-allocator hook cannot turn it into an
+    exception (csrc/arena.cpp stops the process with the sizes)."""
+    pred, basis = predicted_peak_gib(frames, image_size, bf16, resident, lite, key)
+    if pred is None:
+        return
+    from . import arena
+    cap = arena.capacity_gib(device) if arena.active() else 0.0
+    if cap:
+        limit, what = arena_budget * cap, f"{arena_budget:.0%} of the device-memory arena's {cap:.1f} GiB"
+    else:
+        limit = torch.cuda.get_device_properties(device).total_memory / 2 ** 30
+        what = f"the device's {limit:.1f} GiB"
+    if pred > limit:
+        raise RuntimeError(
+            f"memory policy resident_stages={tuple(resident)} lite_stages={tuple(lite)} needs {pred:.1f} GiB "
+            f"({basis}) for {frames} frames of {image_size}x{image_size}, more than {what} ({limit:.1f} GiB); "
+            f"use fewer resident stages (or resident_stages='auto')")
 
 
 def auto_resident_stages(frames, image_size, bf16, device, budget=0.85, key=((2, 2, 6, 2), 4),

@@ -48,7 +48,10 @@ def test_torch_library_registration():
              "dwconv_s2_bn_bwd": "dwconv_bn_bwd"}   # ssl_mae::dwconv_bn_bwd dispatches on stride
     internal = {"add",                       # not used by the step
                 "bn_stats_from_partials",    # the statistics step inside ssl_mae::dwconv_fused
-                "gemm_persistent"}           # a host-side mode switch, no compute
+                "gemm_persistent",           # a host-side mode switch, no compute
+                "gemm_tuning",               # A/B knobs of the GEMM dispatch (scripts only), no compute
+                "attn_tuning",               # A/B switch of the attention backward's MFMA shape, no compute
+                "calibrate_mfma"}            # bench.py's box calibration loop, not a step op
     for sym in _lib.exported_symbols():
         base = sym[3:]
         if base.endswith(("_workspace_bytes", "_partial_rows")) or base in internal:

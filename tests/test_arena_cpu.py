@@ -120,3 +120,40 @@ def test_small_stage0_resident_needs_arena(monkeypatch, cap, expect):
     monkeypatch.setattr(arena, "capacity_gib", lambda d=None: cap)
     assert TV.auto_resident_stages(256 * 8, 224, True, "cuda", key=((2, 2, 12, 2), 8)) == expect
     assert TV.auto_lite_stages(256 * 8, 224, True, "cuda", expect, key=((2, 2, 12, 2), 8)) == ()
+
+
+def test_explicit_policy_checked_against_arena_capacity(monkeypatch):
+    """An explicit resident / lite request whose predicted peak exceeds the arena's capacity
+    raises a RuntimeError naming both sizes before the step (instead of the arena meeting the
+    failing request inside the step, csrc/arena.cpp); the capacity is read from a host-attached
+    arena slot.  C3 ViT-Small with stage 2 resident was measured out of memory at > 300 GB."""
+    from ssl_mae_amd import tiny_vit as TV
+    slot = 12
+    _attach(slot, int(281.4 * 2 ** 30))
+    monkeypatch.setattr(arena, "active", lambda: True)
+    small, tiny = ((2, 2, 12, 2), 8), ((2, 2, 6, 2), 4)
+    F, S = 256 * 8, 224
+    with pytest.raises(RuntimeError, match=r"needs 279\.4 GiB") as ei:
+        TV.check_memory_policy(F, S, True, slot, (2,), (), key=small)
+    msg = str(ei.value)
+    assert "lower bound" in msg and "281.4 GiB" in msg and "arena" in msg
+    with pytest.raises(RuntimeError, match="lower bound"):          # a superset of an OOM policy
+        TV.check_memory_policy(F, S, True, slot, (1, 2), (), key=small)
+    TV.check_memory_policy(F, S, True, slot, (0,), (), key=small)    # 231.2 GiB measured: fits
+    TV.check_memory_policy(F, S, True, slot, (0, 1, 2), (), key=tiny)   # 263.1 GiB: fits
+    TV.check_memory_policy(F, S, True, slot, (1, 2), (0,), key=tiny)    # 229.8 GiB: fits
+    TV.check_memory_policy(64, S, True, slot, (2,), (), key=small)   # small batches always fit
+    with pytest.raises(RuntimeError, match="measured"):               # fp32 doubles the activations
+        TV.check_memory_policy(F, S, False, slot, (0, 1, 2), (), key=tiny)
+    pred, basis = TV.predicted_peak_gib(F, S, True, (1,), (), key=small)
+    assert basis == "estimate" and 184.0 < pred < 288.0
+    assert TV.predicted_peak_gib(F, S, True, (0,), key=((9, 9, 9, 9), 1)) == (None, None)
+
+
+def test_stats_device_index_bounds():
+    """sm_arena_stats / sm_arena_reset_peak ignore out-of-range device slots."""
+    lib = arena.library()
+    out = (ctypes.c_uint64 * 8)(*([7] * 8))
+    lib.sm_arena_stats(99, out)
+    assert list(out) == [0] * 8
+    lib.sm_arena_reset_peak(-1)

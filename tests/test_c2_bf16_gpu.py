@@ -83,7 +83,7 @@ def _head_ref(qkv, dO, n, h, N, L, H, D, p, seed):
     q, k, v = [t[:, i, :].clone().requires_grad_(True) for i in range(3)]
     P = torch.softmax((q @ k.t()) / math.sqrt(D), -1)
     if p > 0:
-        P = P * _attn_keep(n, h, H, L, p, seed) / (1 - p)
+        P = P * _attn_keep(n, h, H, L, p, seed) * (128 / (128 - int(p * 128 + 0.5)))   # attn_drop_scale
     o = P @ v
     do = dO.view(N, L, H, D)[n, :, h, :].float()
     o.backward(do)

@@ -37,6 +37,14 @@ def rel_err(a, b):
 TOL = {torch.float32: 2e-5, torch.bfloat16: 2e-2}
 
 
+def drop_scale(p, attn=False):
+    """Kept-value scale of the counter-hash dropout (csrc/common.h drop_scale, attention.hip
+    attn_drop_scale): the inverse of the quantised keep rate, 256 / (256 - round(256 p)) or
+    128 / (128 - round(128 p)), so E[mask * scale] = 1 as nn.Dropout."""
+    q = 128 if attn else 256
+    return q / (q - int(p * q + 0.5))
+
+
 def rnd(*shape, dtype=torch.float32, scale=1.0, seed=0):
     g = torch.Generator().manual_seed(seed)
     return (torch.randn(*shape, generator=g) * scale).to(dtype)
@@ -233,7 +241,7 @@ def test_attention_dropout_exact_mask(dtype, D, L):
     rows = np.arange(N * H * L)
     keep = torch.from_numpy(_np_keep(rows, np.arange(L), p, seed, attn=True)).reshape(N, H, L, L)
     P = torch.softmax((q @ k.transpose(-1, -2)) / math.sqrt(D), -1)
-    o_ref = (P * keep / (1 - p)) @ v
+    o_ref = (P * keep * drop_scale(p, attn=True)) @ v
     o_ref_flat = o_ref.transpose(1, 2).reshape(N * L, H * D)
     o_ref_flat.backward(dO.float())
     dqkv_ref = torch.stack([q.grad, k.grad, v.grad]).permute(1, 3, 0, 2, 4).reshape(N * L, 3 * H * D)
@@ -639,7 +647,7 @@ def test_adamw_matches_torch():
 
 def test_dropout_masks_fwd_bwd_consistent():
     """GEMM-epilogue dropout, GELU dropout and their backward kernels regenerate the
-    same counter-hash mask; keep rate ~ 1-p; kept entries scaled by 1/(1-p)."""
+    same counter-hash mask; keep rate ~ 1-p; kept entries scaled by 256/(256-round(256p))."""
     kk = KK()
     M, N, Kd, p, seed = 512, 384, 64, 0.1, 1234
     x = rnd(M, Kd, dtype=torch.bfloat16, seed=1).to(DEV)
@@ -650,7 +658,7 @@ def test_dropout_masks_fwd_bwd_consistent():
     ratio = (y / y0).cpu()
     kept = (ratio.abs() > 0.5)
     assert abs(kept.float().mean().item() - (1 - p)) < 0.01
-    assert torch.allclose(ratio[kept], torch.full_like(ratio[kept], 1 / (1 - p)), rtol=1e-3)
+    assert torch.allclose(ratio[kept], torch.full_like(ratio[kept], drop_scale(p)), rtol=1e-3)
     g = kk.dropout_bwd(torch.ones(M, N, dtype=torch.float32, device=DEV), p, seed).cpu()
     assert torch.equal(g > 0, kept)
     pre = rnd(M, N, dtype=torch.bfloat16, seed=3).to(DEV)
@@ -661,7 +669,7 @@ def test_dropout_masks_fwd_bwd_consistent():
     assert torch.equal((d != 0) | (h0 == 0), km)
     s = kk.droppath_scale(10000, 0.1, 7, DEV).cpu()
     vals = torch.unique(s)
-    assert len(vals) == 2 and vals[0] == 0 and abs(vals[1].item() - 1 / 0.9) < 1e-6
+    assert len(vals) == 2 and vals[0] == 0 and abs(vals[1].item() - drop_scale(0.1)) < 1e-6
     assert abs((s > 0).float().mean() - 0.9) < 0.02
 
 
@@ -681,7 +689,7 @@ def test_linear_dx_gelu_backward_epilogue(dtype, p):
     assert rel_err(got, ref2) < tol
     keep = (kk.gelu(pre, p, seed).float() != 0) | (kk.gelu(pre).float() == 0)
     pr = pre.float().requires_grad_(True)
-    h = F.gelu(pr) * keep / (1 - p)
+    h = F.gelu(pr) * keep * drop_scale(p)
     h.backward(dy.float() @ w.float())
     assert rel_err(got, pr.grad) < tol
 
@@ -785,7 +793,7 @@ def test_linear_dw_bias_gelu_operand(M, N, H, p):
     kk.linear_dw_bias(dy, pre, gw2, gb2, gelu=(p, 99))
     assert torch.equal(gw1, gw2) and torch.equal(gb1, gb2)
     keep = ((h.float() != 0) | (kk.gelu(pre).float() == 0)).float()
-    ref = dy.float().t() @ (F.gelu(pre.float()) * keep / (1 - p))
+    ref = dy.float().t() @ (F.gelu(pre.float()) * keep * drop_scale(p))
     assert rel_err(gw2, ref) < 2e-2
 
 
