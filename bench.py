@@ -44,6 +44,9 @@ def parse():
     ap.add_argument("--size", type=int, default=224)
     ap.add_argument("--mask-ratio", type=float, default=0.75)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--attn-bwd-shape", default="",
+                    help="A/B only: MFMA shape of the bf16 attention backward as 'D64,D32' (16 or 32 each; "
+                         "default: the library's); reported in config when given")
     ap.add_argument("--no-calibration", action="store_true",
                     help="skip the box calibration (bare MFMA loops + a 4.9 GB copy) before the timed steps")
     ap.add_argument("--resident", default="",
@@ -150,7 +153,8 @@ def calibration(dev, copy_gb=4.9):
 
 
 PROBE_KERNELS = {"dec_attn_fwd": "attn_fwd_bf16<64, true>",
-                 "dec_attn_bwd": "attn_bwd_dq_bf16<64, true, 4>+attn_bwd_dkdv_bf16<64, true, 4>"}
+                 "dec_attn_bwd": "attn_bwd_dq_bf16<64, true, 4>+attn_bwd_dkdv_bf16<64, true, 4>",
+                 "dec_attn_bwd16": "attn_bwd_dq16_bf16<64, true, 4>+attn_bwd_dkdv16_bf16<64, true, 4>"}
 def reference_cpu():
     """The reference's own train_one_epoch timed on the build container's CPU cores at
     BASELINE config 1 by scripts/ref_cpu_baseline.py (the reference cannot travel to
@@ -165,6 +169,15 @@ def reference_cpu():
         out["source"] = os.path.relpath(f, ROOT)
         return out
     return None
+
+
+def probe_kernel_key(probe):
+    """PROBE_KERNELS key of the kernels the probe times: the decoder backward's kernel pair
+    depends on the MFMA shape selected for head dim 64 (sm_attn_tuning)."""
+    if probe == "dec_attn_bwd":
+        from ssl_mae_amd import kernels as K
+        return "dec_attn_bwd16" if K.attn_tuning(64) == 16 else "dec_attn_bwd"
+    return probe
 
 
 def pmc_traffic(probe, B, T, S):
@@ -183,7 +196,7 @@ def pmc_traffic(probe, B, T, S):
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if d.get("kernel") == PROBE_KERNELS.get(probe):
+        if d.get("kernel") == PROBE_KERNELS.get(probe_kernel_key(probe)):
             return {"traffic": round(d["traffic_bytes"] / 1e9, 3), "traffic_unit": "GB/launch",
                     "algorithmic_gb_per_launch": round(algo[probe] / 1e9, 3),
                     "traffic_source": os.path.relpath(f, ROOT)}
@@ -315,6 +328,9 @@ def main():
         loss, _, _ = train_step(model, clips[i % 2], opt, scaler, ssl_cfg, bf16=True)
         return loss
 
+    if args.attn_bwd_shape:
+        for D, v in zip((64, 32), args.attn_bwd_shape.split(",")):
+            K.attn_tuning(D, int(v))
     if args.resident or args.lite:   # an explicit policy must fit before the first step (RuntimeError)
         enc = model.encoder
         TV.check_memory_policy(B * T, S, True, dev, resident_used(model, B * T, S), lite_used(model, B * T, S),
@@ -371,7 +387,8 @@ def main():
         avg = probe.avg_ms()
         if avg and flop_per_launch:
             achieved = flop_per_launch / (avg * 1e-3) / 1e12
-            roof = {"kernel": args.probe, "bound": "mfma", "achieved": round(achieved, 1),
+            roof = {"kernel": args.probe, "kernels": PROBE_KERNELS.get(probe_kernel_key(args.probe)),
+                    "bound": "mfma", "achieved": round(achieved, 1),
                     "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None,
                     "avg_launch_ms": round(avg, 3), "launches": len(probe.pairs),
@@ -415,7 +432,8 @@ def main():
                        "parallelism": f"dp{world}",
                        "resident_stages": list(resident_used(model, B * T, S)),
                        "lite_stages": lite_used(model, B * T, S),
-                       **({"gemm_tuning": K.gemm_tuning_nondefault()} if K.gemm_tuning_nondefault() else {})},
+                       **({"gemm_tuning": K.gemm_tuning_nondefault()} if K.gemm_tuning_nondefault() else {}),
+                       **({"attn_bwd_shape": args.attn_bwd_shape} if args.attn_bwd_shape else {})},
             "calibration": calib,
             "step_ms_first5": step_ms[:5], "step_ms_last5": step_ms[-5:],
             "roofline": roof,

@@ -1,5 +1,6 @@
 set -e
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_dropout_unbiased_gpu.py tests/test_attn16_gpu.py > gpurun_out/r06b_tests.log 2>&1
-timeout -k 10 300 python scripts/kbench.py attn --bwd-shapes 32,16 --rounds 3 --iters 3 > gpurun_out/r06b_kbench_attn.txt 2>&1
+T=${1:-r06g}
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_kernels_gpu.py -k "stem_conv2_direct" > gpurun_out/${T}_tests.log 2>&1
+timeout -k 10 300 python scripts/kbench.py stem --rounds 3 --iters 5 > gpurun_out/${T}_kbench_stem.txt 2>&1

@@ -1348,11 +1348,12 @@ __global__ __launch_bounds__(128) void attn_bwd_dkdv_f32(AttnArgs a) {
 // pair measured 1-10 % slower, profiles/r04c_attn_bwd_variants.txt.)
 // MFMA shape of the bf16 backward per head dim (sm_attn_tuning: 32 = v_mfma_f32_32x32x16_bf16,
 // 16 = v_mfma_f32_16x16x32_bf16); key 0: D = 64 (decoder), key 1: D = 32 (encoder).
-int g_attn_bwd_shape[2] = {32, 32};
+int g_attn_bwd_shape[2] = {16, 32};   // measured: profiles/r06cd_attn_bwd16_variants.txt
 template <int D, bool DROP>
 void launch_attn_bwd(const AttnArgs& a, hipStream_t st) {
   const dim3 g4((unsigned)((a.L + 127) / 128) * (unsigned)(a.H * a.N));
-  if (g_attn_bwd_shape[D == 64 ? 0 : 1] == 16) {
+  const int shape = g_attn_bwd_shape[D == 64 ? 0 : 1];
+  if (shape == 16) {
     hipLaunchKernelGGL((attn_bwd_dq16_bf16<D, DROP>), g4, dim3(256), 0, st, a);
     hipLaunchKernelGGL((attn_bwd_dkdv16_bf16<D, DROP>), g4, dim3(256), 0, st, a);
     return;
@@ -1428,7 +1429,7 @@ extern "C" int sm_attn_bwd(int dtype, int N, int L, int H, int D, const void* qk
 }
 
 // A/B switch of the bf16 backward's MFMA shape (see launch_attn_bwd): key 0 = D 64, 1 = D 32;
-// *prev <- current shape; set > 0 stores value (16 or 32), set < 0 restores 32.  Host-side only.
+// *prev <- current shape; set > 0 stores value (16 or 32), set < 0 restores the default.  Host-side only.
 extern "C" int sm_attn_tuning(int key, int set, int value, int* prev) {
   if (key < 0 || key > 1) return -2;
   if (prev) *prev = g_attn_bwd_shape[key];
@@ -1436,7 +1437,7 @@ extern "C" int sm_attn_tuning(int key, int set, int value, int* prev) {
     if (value != 16 && value != 32) return -2;
     g_attn_bwd_shape[key] = value;
   } else if (set < 0) {
-    g_attn_bwd_shape[key] = 32;
+    g_attn_bwd_shape[key] = key == 0 ? 16 : 32;
   }
   return 0;
 }

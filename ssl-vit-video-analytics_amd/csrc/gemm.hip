@@ -1323,7 +1323,10 @@ __global__ __launch_bounds__(512, 4) void gemm_bf16_pp(GemmArgs g) {
   };
   // operand staging (TileLoader's chunk map; rows past the matrix clipped by the descriptor's
   // record count (K-major) or an out-of-range offset (M/N-major columns), chunks past K by
-  // the K check; the per-chunk stride is the scalar offset)
+  // the K check).  The K-major chunks' row stride goes in the VGPR offset: the buffer range
+  // check covers voffset (+ the instruction offset) but not the scalar offset on CDNA, so a
+  // chunk i >= 1 of a ragged last tile addressed through soffset would read rows past the
+  // matrix -- past the end of its allocation for an A / B at the end of one.
   uint4 ra[CHA], rb[CHB];
   auto issue = [&](int k0) {
     const int t = opaque_tid();
@@ -1335,7 +1338,7 @@ __global__ __launch_bounds__(512, 4) void gemm_bf16_pp(GemmArgs g) {
     const uint32_t a_v = kk < kv ? (uint32_t)(((t >> 3) * g.lda + kk) * 2) : BUF_OOB;
 #pragma unroll
     for (int i = 0; i < CHA; ++i)
-      ra[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsa, a_v, i * a_rs, 0));
+      ra[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsa, a_v + i * a_rs, 0, 0));
     const int bcols = g.N - ln0 < BNV ? g.N - ln0 : BNV;
     if constexpr (BK) {
       const auto rsb = __builtin_amdgcn_make_buffer_rsrc((void*)(B + (int64_t)ln0 * g.ldb + k0), (short)0,
@@ -1343,7 +1346,7 @@ __global__ __launch_bounds__(512, 4) void gemm_bf16_pp(GemmArgs g) {
       const uint32_t b_v = kk < kv ? (uint32_t)(((t >> 3) * g.ldb + kk) * 2) : BUF_OOB;
 #pragma unroll
       for (int i = 0; i < CHB; ++i)
-        rb[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsb, b_v, i * b_rs, 0));
+        rb[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsb, b_v + i * b_rs, 0, 0));
     } else {
       const auto rsb = panel_rsrc(B, (int64_t)k0 * g.ldb + ln0);
       const int bk = t / (BNV / 8), bc = (t % (BNV / 8)) * 8;

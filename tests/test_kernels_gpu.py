@@ -975,10 +975,11 @@ def test_stem_conv1_direct(shape, frames):
     assert int(nb2) == 1 == int(nb1)
 
 
+@pytest.mark.parametrize("rows", [1, 2])
 @pytest.mark.parametrize("Fn,H,W,gelu", [(3, 14, 12, True), (2, 9, 23, True), (32, 112, 112, True),
                                          (1, 5, 128, True), (2, 1, 7, False), (3, 3, 33, False),
-                                         (2, 7, 110, True), (1, 4, 109, False)])
-def test_stem_conv2_direct(Fn, H, W, gelu):
+                                         (2, 7, 110, True), (1, 4, 109, False), (2, 2, 112, True)])
+def test_stem_conv2_direct(Fn, H, W, gelu, rows):
     """Stem conv2 over act(a1) with BN1 (+GELU) applied in the kernel's LDS ring
     (sm_stem_conv2_bn_stats): y bit-identical to conv3x3_fwd(bn_apply(a1)) (same k order
     and MFMA chain), BN2 statistics / running statistics within fp32 rounding.  Shapes:
@@ -999,7 +1000,11 @@ def test_stem_conv2_direct(Fn, H, W, gelu):
     nb2 = nb1.clone()
     h1 = kk.bn_apply(a1, m1, r1, g1, b1, gelu=gelu)
     y1, mm1, rr1 = kk.conv3x3_fwd_bn_stats(h1, wp, Fn, H, W, 48, 96, rm1, rv1, 0.1, 1e-5, 1, nb1)
-    y2, mm2, rr2 = kk.stem_conv2_bn_stats(a1, (m1, r1, g1, b1, gelu), wp, Fn, H, W, rm2, rv2, 0.1, 1e-5, 1, nb2)
+    prev = kk.stem_tuning(rows)          # band height: 2 rows (three barriers) or 1 row (one barrier)
+    try:
+        y2, mm2, rr2 = kk.stem_conv2_bn_stats(a1, (m1, r1, g1, b1, gelu), wp, Fn, H, W, rm2, rv2, 0.1, 1e-5, 1, nb2)
+    finally:
+        kk.stem_tuning(prev)
     assert torch.equal(y1, y2)
     assert rel_err(mm2, mm1) < 1e-5 and rel_err(rr2, rr1) < 1e-5
     assert rel_err(rm2, rm1) < 1e-5 and rel_err(rv2, rv1) < 1e-5
@@ -1092,3 +1097,38 @@ def test_dwconv_bn_bwd_vs_fp32(Fr, H, C, s):
     assert rel_err(da1, gx) < 2e-2 and rel_err(da1, da1_u) < 2e-2
     assert rel_err(dw_f, tw.grad) < 1e-2 and rel_err(dw_f, dw_u) < 1e-2
     assert rel_err(dg_f, tg.grad) < 2e-2 and rel_err(db_f, tb.grad) < 2e-2
+
+
+@pytest.mark.parametrize("Kd,N", [(96, 392), (384, 520)])
+def test_gemm_persistent_ragged_operands_at_allocation_end(Kd, N):
+    """gemm_bf16_pp with a ragged last m-tile (M % 256 = 77) and a ragged last n-tile whose A and
+    B rows end exactly at the end of their allocations (views onto the tail of a 2-MiB-multiple
+    buffer): every chunk's row is range-checked through its VGPR offset, so rows past M / N
+    read zero instead of memory past the allocation (the scalar-offset form left
+    chunks 1-3 of the last tile unchecked).  Bit-identical to the one-tile-per-block form."""
+    kk = KK()
+    M = 256 * 40 + 77
+
+    def tail_view(rows, cols, seed):
+        n = rows * cols
+        cap = ((n * 2 + (2 << 20) - 1) // (2 << 20)) * (2 << 20) // 2
+        buf = torch.empty(cap, dtype=torch.bfloat16, device=DEV)
+        v = buf[cap - n:].view(rows, cols)
+        v.copy_(rnd(rows, cols, dtype=torch.bfloat16, seed=seed).to(DEV))
+        return v
+
+    x = tail_view(M, Kd, 401)
+    w = tail_view(N, Kd, 402)
+    outs = []
+    prev = kk.gemm_persistent(0)
+    try:
+        for mode in (0, 1):
+            kk.gemm_persistent(mode)
+            out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+            kk.gemm(x, w, out, M, N, Kd, 0, 0, Kd, Kd, N)
+            outs.append(out)
+    finally:
+        kk.gemm_persistent(prev)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    assert rel_err(outs[1], x.float() @ w.float().t()) < TOL[torch.bfloat16]
