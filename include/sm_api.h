@@ -244,11 +244,6 @@ int sm_stem_conv2_bn_stats(const void* a1, int F, int H, int W, const float* bn1
                            const float* bn1_w, const float* bn1_b, int gelu, const void* wpack, void* y, float* mean,
                            float* rstd, float* run_mean, float* run_var, int64_t* num_batches_tracked, float momentum,
                            float eps, int updates, void* ws, int64_t ws_bytes, hipStream_t st);
-/* Band height of sm_stem_conv2_bn_stats' kernel (A/B and tests; the default is the measured
- * best): 2 = two output rows per band, 1 = one row per band with the next row's BN1 + GELU
- * committed beside the MFMAs.  *prev <- current; set > 0 stores value, set < 0 restores the
- * default.  Returns 0, or -2 for another value.  Host-side only. */
-int sm_stem_tuning(int set, int value, int* prev);
 /* Stem conv2 (tiny_vit.py:69, 3x3 / stride 1 / pad 1, bf16, channels-last) as GEMMs over
  * the implicit im2col matrix -- no [pixels][9C] buffer in HBM.  wpack = sm_conv_wpack
  * order 1 ([Cout][9*Cin]); wpack_t = order 2 ([Cin][9*Cout]); Cin, Cout % 8 == 0.

@@ -244,12 +244,8 @@ def stem(args):
     del col
     rep("stem_conv1_bn_stats (direct)", timeit(lambda: K.stem_conv1_bn_stats(clip, w1p), args.iters))
     a1, m1, r1, _ = K.stem_conv1_bn_stats(clip, w1p)
-    for _ in range(args.rounds):   # interleaved rounds of the two band heights
-        for rows in (2, 1):
-            prev = K.stem_tuning(rows)
-            rep(f"stem_conv2_bn_stats (direct, {rows}-row bands)",
-                timeit(lambda: K.stem_conv2_bn_stats(a1, (m1, r1, g1, b1, True), w2p, Fr, Ho, Wo), args.iters))
-            K.stem_tuning(prev)
+    rep("stem_conv2_bn_stats (direct, act in ring)",
+        timeit(lambda: K.stem_conv2_bn_stats(a1, (m1, r1, g1, b1, True), w2p, Fr, Ho, Wo), args.iters))
     rep("bn_apply + GELU (h1)", timeit(lambda: K.bn_apply(a1, m1, r1, g1, b1, gelu=True), args.iters))
     h1 = K.bn_apply(a1, m1, r1, g1, b1, gelu=True)
     rep("conv3x3_fwd_bn_stats", timeit(lambda: K.conv3x3_fwd_bn_stats(h1, w2p, Fr, Ho, Wo, 48, 96), args.iters))

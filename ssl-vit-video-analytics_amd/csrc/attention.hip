@@ -61,6 +61,21 @@ SM_DEV int tile_off(int row, int d) {
   (void)CPR;
 }
 
+// The 16x16x32 kernels' image of the same tile: row reads take rows c = l & 15 at chunk
+// 4 ks + (l >> 4), transposed reads rows 4 (l >> 4) + (c >> 2) at columns 16 dt + 4 (c & 3),
+// which the 32x32x16 swizzle above serves 2-way on both kinds (SQ_LDS_BANK_CONFLICT ~ 1.3x
+// the LDS-active cycles of the first 16x16 build, profiles/r06i_attn_sq.txt).  XORing the
+// chunk with 2 ((row >> 1) & 3) (D = 64: two rows per 256-B bank row) or 2 ((row >> 2) & 1)
+// (D = 32: four) makes every ds_read_b128 lane group and every ds_read_b64_tr_b16 half-wave
+// cover the 64 banks once (checked against the guide's lane groups by enumeration).
+template <int D>
+SM_DEV int tile_off16(int row, int d) {
+  int chunk = d >> 3;
+  if (D == 64) chunk ^= 2 * ((row >> 1) & 3);
+  else chunk ^= ((row >> 2) & 1) << 1;
+  return row * (D * 2) + (chunk << 4) + ((d & 7) << 1);
+}
+
 // combine a value with the lane 32 apart (the other half-wave) by v_permlane32_swap
 // (no LDS round trip): the two results hold {own, other} in either order
 SM_DEV float halves_max(float v) {
@@ -200,7 +215,7 @@ SM_DEV uint32_t quad_transpose_bytes(uint32_t v, uint32_t sel1, uint32_t sel2) {
 // LDS stores after the barrier.  The tile's descriptor (scalar) carries the base
 // and num_records = valid rows x row bytes, so rows past L read as zero with no
 // per-lane address arithmetic, compare or branch in the tile loop.
-template <int D, int ROWS, int NT = 256>
+template <int D, int ROWS, int NT = 256, bool S16 = false>
 struct Stager {
   static constexpr int CH = ROWS * D / 8 / NT;
   static_assert(CH >= 1 && CH * NT * 8 == ROWS * D, "tile must split evenly over the block's threads");
@@ -213,7 +228,7 @@ struct Stager {
       const int c = threadIdx.x + NT * i;
       const int row = c / (D / 8), d = (c % (D / 8)) * 8;
       voff[i] = (uint32_t)(row * ld + d) * 2u;
-      loff[i] = tile_off<D>(row, d);
+      loff[i] = S16 ? tile_off16<D>(row, d) : tile_off<D>(row, d);
     }
   }
   SM_DEV void load(const __bf16* base, int rows_left, uint4 (&r)[CH]) const {
@@ -826,12 +841,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_bf16(AttnArgs a) 
 template <int D>
 SM_DEV int row16_off(int ks) {   // A fragment: 8 consecutive d at k-step ks of row c
   const int l = threadIdx.x & 63;
-  return tile_off<D>(l & 15, 32 * ks + 8 * (l >> 4));
+  return tile_off16<D>(l & 15, 32 * ks + 8 * (l >> 4));
 }
 template <int D>
 SM_DEV int tr16_off(int dt) {    // transposed A fragment (first block): rows 4g + (c>>2), cols 16 dt + 4 (c&3)
   const int l = threadIdx.x & 63, c = l & 15;
-  return tile_off<D>(4 * (l >> 4) + (c >> 2), 16 * dt + 4 * (c & 3));
+  return tile_off16<D>(4 * (l >> 4) + (c >> 2), 16 * dt + 4 * (c & 3));
 }
 SM_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -886,7 +901,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv16_bf16(AttnArgs
       }
     }
   }
-  Stager<D, QT, 64 * NW> sq, sd;
+  Stager<D, QT, 64 * NW, true> sq, sd;
   sq.init(C);
   sd.init(C);
   int roff[KS], toff[DT];
@@ -989,7 +1004,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv16_bf16(AttnArgs
     }
   };
 
-  uint4 rq[Stager<D, QT, 64 * NW>::CH], rd[Stager<D, QT, 64 * NW>::CH];
+  uint4 rq[Stager<D, QT, 64 * NW, true>::CH], rd[Stager<D, QT, 64 * NW, true>::CH];
   float rlse = 0.f, rdel = 0.f;
   auto rowc_load = [&](int q0) {
     if (threadIdx.x < QT) {
@@ -1099,7 +1114,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq16_bf16(AttnArgs a
       if (qok) *(bf16x8*)(a.qc + ((int64_t)n * a.L + q) * C + hd * D + 32 * ks + 8 * g) = qf[qg][ks];
     }
   }
-  Stager<D, KT, 64 * NW> stg;
+  Stager<D, KT, 64 * NW, true> stg;
   stg.init(ldq);
   int roff[KS], toff[DT];
 #pragma unroll
@@ -1121,7 +1136,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq16_bf16(AttnArgs a
     dlb[qg] = seed32(a.seed) + (uint32_t)((uint64_t)(n * a.H + hd) * a.L + qbase + 16 * qg + c) * AG +
               (uint32_t)g * AC;
 
-  uint4 rk[Stager<D, KT, 64 * NW>::CH], rv[Stager<D, KT, 64 * NW>::CH];
+  uint4 rk[Stager<D, KT, 64 * NW, true>::CH], rv[Stager<D, KT, 64 * NW, true>::CH];
   stg.load(kb, a.L, rk);
   stg.load(vb, a.L, rv);
   auto tile = [&](int k0, auto rag) {

@@ -488,146 +488,6 @@ __global__ __launch_bounds__(SC2_NT, 1) void stem_conv2_kernel(const __bf16* a1,
   }
 }
 
-// ------------------------------------------------------------------ stem conv2, one row per band
-// The same convolution (bit-identical y: k order (tap, ci), 16-wide k-steps, MFMA chain
-// ky -> kx -> c16 per output pixel) restructured around one barrier per output row:
-// * the packed weights stay in LDS as stem_conv2_kernel's image; per tap row each wave loads
-//   its 9 fragments (one row per band: 2 ds_read_b128 per MFMA with the pixel fragments);
-// * the ring holds 4 h1 rows: band y reads rows y-1, y, y+1 and, between its tap rows'
-//   MFMAs, commits row y+2 (BN1 + GELU of a1 loaded one band earlier, double-buffered in
-//   registers) into the slot of row y-2, dead since the band's barrier; the transform's VALU
-//   work thereby runs beside the MFMAs instead of in a phase of its own;
-// * the output row leaves through a wave-private 1-KB LDS staging area as 16-B runs of 8
-//   channels (two halves of 16 pixels), with no block barrier.
-// BN2 sums: per lane (channel), pixels in row order as stem_conv2_kernel.
-constexpr int SC3_STG = 1024;
-constexpr int SC3_RING = SC2_NR * SC2_PXS * SC2_PITCH * 2;
-constexpr int SC3_LDS = SC3_RING + SC2_COUT * SC2_WPITCH * 2 + SC2_NW * SC3_STG;
-static_assert(SC2_NR == 4, "one-row bands read 3 ring rows and commit a 4th");
-
-template <bool GELU>
-__global__ __launch_bounds__(SC2_NT, 1) void stem_conv2r_kernel(const __bf16* a1, ChanAffine act,
-                                                                const __bf16* wpack /*[96][432]*/, __bf16* y,
-                                                                float* part /*[F][2][96]*/, int H, int W) {
-  __shared__ __attribute__((aligned(16))) char lds[SC3_LDS];
-  __shared__ float aff[2][SC2_CIN];
-  __shared__ float red[SC2_NW][2][32];
-  __bf16* ring = (__bf16*)lds;
-  __bf16* wl = (__bf16*)(lds + SC3_RING);
-  const int t = threadIdx.x, l = t & 63, h = l >> 5, wv = t >> 6;
-  const int nb = wv % 3, sg = wv / 3;
-  char* stg = lds + SC3_RING + SC2_COUT * SC2_WPITCH * 2 + wv * SC3_STG;
-  const int64_t f = blockIdx.x;
-  const __bf16* src = a1 + f * H * W * SC2_CIN;
-  if (t < SC2_CIN) {   // = Affine8::init
-    const float sc = act.rstd[t] * act.w[t];
-    aff[0][t] = sc;
-    aff[1][t] = bn_shift(act.b[t], act.mean[t], sc);
-  }
-  for (int i = t; i < SC3_RING / 16; i += SC2_NT) *(uint4*)(lds + 16 * i) = make_uint4(0, 0, 0, 0);
-  for (int i = t; i < SC2_COUT * SC2_K / 8; i += SC2_NT) {
-    const int c = i / (SC2_K / 8), k8 = i - c * (SC2_K / 8);
-    *(uint4*)(wl + c * SC2_WPITCH + 8 * k8) = *(const uint4*)(wpack + c * SC2_K + 8 * k8);
-  }
-  // this wave's weight row: channel co = 32 nb + (l & 31), k = 16 q + 8 h (q = 9 ky + 3 kx + c16)
-  const int co = 32 * nb + (l & 31);
-  const __bf16* wrow = wl + co * SC2_WPITCH + 8 * h;
-  // this thread's chunk of a row: pixel x, 8-channel group cc (W * 6 <= 768 chunks)
-  const bool cact = t < W * (SC2_CIN / 8);
-  const int cx = t / (SC2_CIN / 8), ccg = t - cx * (SC2_CIN / 8);
-  auto slot = [&](int iy) { return (iy + 1) & 3; };
-  auto load_row = [&](int iy) {
-    uint4 r = make_uint4(0, 0, 0, 0);
-    if (cact && iy < H) r = *(const uint4*)(src + ((int64_t)iy * W + cx) * SC2_CIN + 8 * ccg);
-    return r;
-  };
-  auto commit = [&](const uint4& r, int iy) {   // BN1 + GELU (= bn_apply) into the row's slot; past H: zero
-    if (!cact) return;
-    float vv[8];
-    load8((const __bf16*)&r, vv);
-#pragma unroll
-    for (int j = 0; j < 8; j += 2) {
-      f32x2 u = vfma(f32x2{vv[j], vv[j + 1]}, f32x2{aff[0][8 * ccg + j], aff[0][8 * ccg + j + 1]},
-                     f32x2{aff[1][8 * ccg + j], aff[1][8 * ccg + j + 1]});
-      if (GELU) u = gelu_f2(u);
-      vv[j] = iy < H ? u.x : 0.f;
-      vv[j + 1] = iy < H ? u.y : 0.f;
-    }
-    store8(ring + (slot(iy) * SC2_PXS + cx + 1) * SC2_PITCH + 8 * ccg, vv);
-  };
-  __syncthreads();   // aff, zeroed ring
-  commit(load_row(0), 0);
-  commit(load_row(1), 1);
-  uint4 raw[2];
-  raw[0] = load_row(2);   // committed during band 0
-  float s1 = 0.f, s2 = 0.f;
-  const int pxl = sg * 32 + (l & 31);   // this lane's A-fragment pixel (output column)
-  auto band = [&](int yo, const uint4& cur, uint4& nxt) {
-    __syncthreads();   // band yo - 1 read its rows (slot of yo + 2 is free); row yo + 1 is visible
-    nxt = load_row(yo + 3);
-    f32x16 acc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-#pragma unroll
-    for (int ky = 0; ky < 3; ++ky) {
-      const __bf16* rp = ring + (slot(yo + ky - 1) * SC2_PXS + pxl) * SC2_PITCH + 8 * h;
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx)
-#pragma unroll
-        for (int c16 = 0; c16 < 3; ++c16)
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*(const bf16x8*)(rp + kx * SC2_PITCH + 16 * c16),
-                                                        *(const bf16x8*)(wrow + 16 * (9 * ky + 3 * kx + c16)),
-                                                        acc, 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);   // one tap row's fragments in flight
-      if (ky == 0) {
-        commit(cur, yo + 2);   // VALU beside the queued MFMAs
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    // lane = channel co, registers = pixels (r & 3) + 8 (r >> 2) + 4 h of the segment; two
-    // halves of 16 pixels through the wave's staging area: lane l reads pixel (l >> 2),
-    // channels 8 (l & 3) .. + 7 of its 32 and stores them as one 16-B run
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-#pragma unroll
-      for (int r = 8 * half; r < 8 * half + 8; ++r) {
-        const int pp = (r & 3) + 8 * (r >> 2) + 4 * h;
-        const __bf16 o = (__bf16)acc[r];
-        *(__bf16*)(stg + (pp - 16 * half) * 64 + (l & 31) * 2) = o;
-        if (sg * 32 + pp < W) {
-          const float of = (float)o;
-          s1 += of;
-          s2 = fmaf(of, of, s2);
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      const int px = (l >> 2) + 16 * half;
-      const uint4 v = *(const uint4*)(stg + (l >> 2) * 64 + (l & 3) * 16);
-      if (sg * 32 + px < W)
-        *(uint4*)(y + ((f * H + yo) * W + sg * 32 + px) * SC2_COUT + 32 * nb + 8 * (l & 3)) = v;
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  int yo = 0;
-  for (; yo + 1 < H; yo += 2) {   // raw[] alternates: static register indices
-    band(yo, raw[0], raw[1]);
-    band(yo + 1, raw[1], raw[0]);
-  }
-  if (yo < H) band(yo, raw[0], raw[1]);
-  s1 += __shfl_xor(s1, 32, 64);
-  s2 += __shfl_xor(s2, 32, 64);
-  if (h == 0) {
-    red[wv][0][l] = s1;
-    red[wv][1][l] = s2;
-  }
-  __syncthreads();
-  if (t < 2 * SC2_COUT) {
-    const int which = t / SC2_COUT, c = t % SC2_COUT, b3 = c / 32, cl = c % 32;
-    part[(f * 2 + which) * SC2_COUT + c] =
-        ((red[b3][which][cl] + red[3 + b3][which][cl]) + red[6 + b3][which][cl]) + red[9 + b3][which][cl];
-  }
-}
-
 // ------------------------------------------------------------------ 3x3 im2col (NHWC)
 template <typename T>
 __global__ void im2col3_kernel(const T* x, int F, int H, int W, int C, int Ho, int Wo, int stride,
@@ -2045,19 +1905,7 @@ extern "C" int sm_stem_conv1_bn_stats(const float* clip, int B, int T, int H, in
                                    momentum, eps, updates, fin, 2 * SC1_COUT * 8, st);
 }
 
-// stem conv2 over GELU(BN1(a1)) + BN2 statistics (see stem_conv2_kernel / stem_conv2r_kernel;
-// sm_stem_tuning selects the band height: 2 = LDS weight image, 1 = register weights)
-int g_stem_conv2_rows = 2;
-extern "C" int sm_stem_tuning(int set, int value, int* prev) {
-  if (prev) *prev = g_stem_conv2_rows;
-  if (set > 0) {
-    if (value != 1 && value != 2) return -2;
-    g_stem_conv2_rows = value;
-  } else if (set < 0) {
-    g_stem_conv2_rows = 2;
-  }
-  return 0;
-}
+// stem conv2 over GELU(BN1(a1)) + BN2 statistics (see stem_conv2_kernel)
 extern "C" int64_t sm_stem_conv2_workspace_bytes(int F) { return (int64_t)F * 2 * SC2_COUT * 4 + 2 * SC2_COUT * 8 + 64; }
 extern "C" int sm_stem_conv2_bn_stats(const void* a1, int F, int H, int W, const float* bn1_mean,
                                       const float* bn1_rstd, const float* bn1_w, const float* bn1_b, int gelu,
@@ -2074,7 +1922,6 @@ extern "C" int sm_stem_conv2_bn_stats(const void* a1, int F, int H, int W, const
   const bool staged = (int64_t)(W + 1) * SC2_PITCH * 2 >= SC2_PITCH * 2 + (SC2_NW / 2) * 2048;
   auto kern = gelu ? (staged ? stem_conv2_kernel<true, true> : stem_conv2_kernel<true, false>)
                    : (staged ? stem_conv2_kernel<false, true> : stem_conv2_kernel<false, false>);
-  if (g_stem_conv2_rows == 1) kern = gelu ? stem_conv2r_kernel<true> : stem_conv2r_kernel<false>;
   hipLaunchKernelGGL(kern, dim3(F), dim3(SC2_NT), 0, st, (const __bf16*)a1,
                      ChanAffine{bn1_mean, bn1_rstd, bn1_w, bn1_b, gelu}, (const __bf16*)wpack, (__bf16*)y, part, H, W);
   SM_CHECK_LAUNCH();

@@ -27,7 +27,6 @@ _SIGS = {
     "sm_gemm_persistent": (_c_i32, [_c_i32]),
     "sm_gemm_tuning": (_c_i32, [_c_i32, _c_i32, _c_i32, _c_p]),
     "sm_attn_tuning": (_c_i32, [_c_i32, _c_i32, _c_i32, _c_p]),
-    "sm_stem_tuning": (_c_i32, [_c_i32, _c_i32, _c_p]),
     "sm_calibrate_mfma": (_c_i32, [_c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p]),
     "sm_gemm": (_c_i32, [_c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_i64, _c_p, _c_i64,
                          _c_p, _c_i64, _c_p, _c_f32, _c_f32, _c_i32, _c_p, _c_p, _c_f32, _c_u64, _c_p, _c_i64,

@@ -283,17 +283,6 @@ def attn_tuning(D, shape=None, reset=False):
     return prev.value
 
 
-def stem_tuning(rows=None, reset=False):
-    """Band height of the stem conv2 kernel (sm_stem_tuning): 2 = stem_conv2_kernel (two output
-    rows per band, three barriers), 1 = stem_conv2r_kernel (one row per band, one barrier, the
-    next row's BN1 + GELU beside the MFMAs).  Returns the current value, then stores `rows`
-    (or the default with reset=True).  Tests and A/B scripts only."""
-    import ctypes
-    prev = ctypes.c_int(0)
-    call("sm_stem_tuning", -1 if reset else (1 if rows is not None else 0), int(rows or 0), ctypes.addressof(prev))
-    return prev.value
-
-
 def attn_fwd(qkv, N, L, H, D, drop_p=0.0, seed=0):
     _chk(qkv)
     out = torch.empty((N * L, H * D), dtype=qkv.dtype, device=qkv.device)

@@ -51,7 +51,6 @@ def test_torch_library_registration():
                 "gemm_persistent",           # a host-side mode switch, no compute
                 "gemm_tuning",               # A/B knobs of the GEMM dispatch (scripts only), no compute
                 "attn_tuning",               # A/B switch of the attention backward's MFMA shape, no compute
-                "stem_tuning",               # A/B switch of the stem conv2 band height, no compute
                 "calibrate_mfma"}            # bench.py's box calibration loop, not a step op
     for sym in _lib.exported_symbols():
         base = sym[3:]
