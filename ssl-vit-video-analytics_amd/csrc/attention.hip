@@ -1447,12 +1447,13 @@ extern "C" int sm_attn_bwd(int dtype, int N, int L, int H, int D, const void* qk
 // *prev <- current shape; set > 0 stores value (16 or 32), set < 0 restores the default.  Host-side only.
 extern "C" int sm_attn_tuning(int key, int set, int value, int* prev) {
   if (key < 0 || key > 1) return -2;
-  if (prev) *prev = g_attn_bwd_shape[key];
+  int& v = g_attn_bwd_shape[key];
+  if (prev) *prev = v;
   if (set > 0) {
     if (value != 16 && value != 32) return -2;
-    g_attn_bwd_shape[key] = value;
+    v = value;
   } else if (set < 0) {
-    g_attn_bwd_shape[key] = key == 0 ? 16 : 32;
+    v = key == 0 ? 16 : 32;
   }
   return 0;
 }
