@@ -71,15 +71,17 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(T, S, ratio, sweep=((1, 16), (1, 64), (4, None))):
+def cpu_baseline(T, S, ratio, sweep=((1, 16), (1, None)), budget_s=30.0):
     """The CPU oracle (fp32 restatement of the reference path, oracle/mae_oracle.py) timed on
-    the GPU box's host cores: one fwd+bwd+AdamW step of the reference's C1 step
+    the GPU box's host cores: one fwd+bwd+AdamW step of the reference's C1 step shape
     (train_ssl_mae.py:66-91, T=8, 224^2) per (clips, threads) point of `sweep` (None = every
     CPU of the process's affinity set), with dropout / DropPath on as the reference ships them
     (attention probabilities materialised per head, as nn.MultiheadAttention's math path),
-    after an untimed small warm-up step per thread count.  The headline value is the
-    reference's own C1 batch (B = 4) on all affinity CPUs; the B = 1 points show the thread
-    scaling at 16 (the box's default OMP share) and 64 threads.  ~40-60 s in total."""
+    after an untimed small warm-up step per thread count.  A bounded sample (one clip per
+    point; the reference's 4-clip C1 batch takes minutes on 16 threads): points after the
+    first run only while the sweep has used less than `budget_s`.  The headline value is the
+    last point measured (all affinity CPUs when it ran); the reference's own B = 4 step is
+    cpu_baseline_reference.  ~20-40 s in total."""
     from oracle import mae_oracle as O
     from ssl_mae_amd.init_rule import param_value, synthetic_clip
     cfg = {"dataset": {"clip_len": T, "image_size": S},
@@ -92,9 +94,13 @@ def cpu_baseline(T, S, ratio, sweep=((1, 16), (1, 64), (4, None))):
     threads0 = torch.get_num_threads()
     wcfg = dict(cfg, dataset={"clip_len": 2, "image_size": 64})
     points = []
+    t_start = time.perf_counter()
     try:
         for B, th in sweep:
+            if points and time.perf_counter() - t_start > budget_s:
+                break
             th = affinity if th is None else min(th, affinity)
+            print(f"[bench] cpu baseline: {B} clip(s) on {th} threads", file=sys.stderr, flush=True)
             torch.set_num_threads(th)
             torch.manual_seed(42)
             wP = O.make_params(wcfg, param_value)
@@ -116,10 +122,10 @@ def cpu_baseline(T, S, ratio, sweep=((1, 16), (1, 64), (4, None))):
     head = points[-1]
     return {"value": head["clips_per_s"], "unit": "clips/s", "cores": head["threads"], "threads": head["threads"],
             "nproc": os.cpu_count(), "affinity_cpus": affinity, "kind": "port", "sweep": points,
-            "sample": f"BASELINE config 1 step: one fp32 fwd+bwd+AdamW step of oracle/mae_oracle.py on {head['clips']} "
-                      f"clips ({T}x3x{S}x{S}) with dropout / DropPath on (as the reference), after a small warm-up "
-                      f"step, on {head['threads']} torch threads = every CPU of the process's affinity set (nproc "
-                      f"{os.cpu_count()}); 'sweep' adds 1-clip steps at 16 and 64 threads; {head['s_per_step']} s"}
+            "sample": f"BASELINE config 1 step shape: one fp32 fwd+bwd+AdamW step of oracle/mae_oracle.py on "
+                      f"{head['clips']} clip(s) ({T}x3x{S}x{S}) with dropout / DropPath on (as the reference), after a "
+                      f"small warm-up step, on {head['threads']} torch threads (affinity set {affinity} CPUs, nproc "
+                      f"{os.cpu_count()}); 'sweep' lists every thread count measured; {head['s_per_step']} s"}
 
 
 def calibration(dev, copy_gb=4.9):
@@ -338,7 +344,13 @@ def main():
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
-    calib = calibration(dev) if not args.no_calibration else None
+    print(f"[bench] {args.warmup} warm-up steps done", file=sys.stderr, flush=True)
+    calib = None
+    if not args.no_calibration:
+        try:
+            calib = calibration(dev)
+        except Exception as e:   # the calibration must not cost the bench line
+            calib = {"error": repr(e)[:200]}
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -352,6 +364,8 @@ def main():
         # train_ssl_mae.py:91): so does the timed loop
         loss_vals.append(float(step(i).item()))
         step_end.append(time.perf_counter())
+        if rank == 0 and (i + 1) % 10 == 0:
+            print(f"[bench] {i + 1}/{args.steps} timed steps", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     probe.active = False
