@@ -862,7 +862,7 @@ SM_DEV uint2 pack4(float a, float b, float c, float d) { return make_uint2(pack_
 // as B fragments per key group and dV^T / dK^T += dO^T P, Qc^T dS over 16-wide d tiles.
 // Row constants, dropout (quad byte transpose: the four keys of a hash are the four lanes
 // of a DPP quad) and the pipelined order are the 32x32x16 kernel's.
-template <int D, bool DROP, int NW = 4, int IG = -1>   // IG >= 0: iglp_opt(IG) scheduling hint (A/B)
+template <int D, bool DROP, int NW = 4>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv16_bf16(AttnArgs a) {
   constexpr int QT = 64;
   constexpr int RB = 16 * D * 2;   // bytes of 16 tile rows
@@ -1032,7 +1032,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv16_bf16(AttnArgs
       rowc_load(q0 + QT);
     }
     if (!wact) continue;
-    if constexpr (IG >= 0) __builtin_amdgcn_iglp_opt(IG);
     f32x4 s0[2][2], p0[2][2], s1[2][2], p1[2][2];
     bf16x8 pf0[2], sf0[2], pf1[2], sf1[2];
     sdp(0, s0, p0);
@@ -1061,7 +1060,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv16_bf16(AttnArgs
 // half s the 2 x 2 (key group, query group) blocks of S^T, dP^T, then dS^T packed per
 // query group and dQ^T += K^T dS^T over 16-wide d tiles.  The prologue forms Delta and
 // writes bf16(Q scale log2 e) for the dK/dV kernel, as the 32x32x16 kernel.
-template <int D, bool DROP, int NW = 4, int IG = -1>
+template <int D, bool DROP, int NW = 4>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq16_bf16(AttnArgs a) {
   constexpr int KT = 64;
   constexpr int RB = 16 * D * 2;
@@ -1151,7 +1150,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq16_bf16(AttnArgs a
       stg.load(vb + (int64_t)(k0 + KT) * ldq, a.L - k0 - KT, rv);
     }
     if (!wact) return;
-    if constexpr (IG >= 0) __builtin_amdgcn_iglp_opt(IG);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       if (RAGGED && s == 1 && k0 + 32 >= a.L) continue;   // no key below L in this half
@@ -1370,16 +1368,6 @@ template <int D, bool DROP>
 void launch_attn_bwd(const AttnArgs& a, hipStream_t st) {
   const dim3 g4((unsigned)((a.L + 127) / 128) * (unsigned)(a.H * a.N));
   const int shape = g_attn_bwd_shape[D == 64 ? 0 : 1];
-  if (shape == 18 || shape == 19) {   // A/B: iglp_opt(0 / 1) in both 16x16x32 kernels
-    if (shape == 18) {
-      hipLaunchKernelGGL((attn_bwd_dq16_bf16<D, DROP, 4, 0>), g4, dim3(256), 0, st, a);
-      hipLaunchKernelGGL((attn_bwd_dkdv16_bf16<D, DROP, 4, 0>), g4, dim3(256), 0, st, a);
-    } else {
-      hipLaunchKernelGGL((attn_bwd_dq16_bf16<D, DROP, 4, 1>), g4, dim3(256), 0, st, a);
-      hipLaunchKernelGGL((attn_bwd_dkdv16_bf16<D, DROP, 4, 1>), g4, dim3(256), 0, st, a);
-    }
-    return;
-  }
   if (shape == 16) {
     hipLaunchKernelGGL((attn_bwd_dq16_bf16<D, DROP>), g4, dim3(256), 0, st, a);
     hipLaunchKernelGGL((attn_bwd_dkdv16_bf16<D, DROP>), g4, dim3(256), 0, st, a);
@@ -1462,7 +1450,7 @@ extern "C" int sm_attn_tuning(int key, int set, int value, int* prev) {
   int& v = g_attn_bwd_shape[key];
   if (prev) *prev = v;
   if (set > 0) {
-    if (value != 16 && value != 32 && value != 18 && value != 19) return -2;   // 18, 19: A/B
+    if (value != 16 && value != 32) return -2;
     v = value;
   } else if (set < 0) {
     v = key == 0 ? 16 : 32;

@@ -345,6 +345,51 @@ def test_bf16_step_t8_224_vs_reference_golden(golden_dir):
     assert n > 150
 
 
+@pytest.mark.timeout(900)
+def test_bf16_step_c1_batch_vs_oracle():
+    """gradients of the timed bf16 kernels anchored above B = 1.  One bf16
+    step at BASELINE C1's batch (B = 4 clips of 8 x 224^2: batch-statistic BatchNorm over four
+    clips' frames, the tube mask of four samples) against the oracle's fp32 gradients of the same
+    step on the same clips and mask (oracle/mae_oracle.py, pinned to the reference by the
+    reference-run fixtures incl. step_b1_t8_s224.npz).  Per parameter tensor: cosine > 0.98 and
+    norm within 10 %, the tolerance of the B = 1 anchor above; the loss within 2 %."""
+    from oracle import mae_oracle as O
+    from ssl_mae_amd.init_rule import param_value, synthetic_clip
+    from ssl_mae_amd.optim import FusedAdamW, GradScaler
+    from ssl_mae_amd.train_ssl_mae import train_step
+    B, T, S, r = 4, 8, 224, 0.75
+    cfg = _cfg(B, T, S, r)
+    model = _model(cfg)
+    opt = FusedAdamW(model.parameters(), lr=5e-4, weight_decay=0.05)
+    clip = torch.from_numpy(synthetic_clip(B, T, S, seed=21)).to(DEV)
+    torch.manual_seed(42)
+    loss, _, idx = train_step(model, clip, opt, GradScaler(), cfg["ssl"], bf16=True)
+    torch.cuda.synchronize()
+    L = (S // 8) ** 2
+    mask = torch.zeros(B * T * L, dtype=torch.bool)
+    mask[idx.long().cpu()] = True
+    mask = mask.reshape(B, T, L)
+    assert int(mask[:, 0].sum()) == B * int(r * L)
+    torch.set_num_threads(max(torch.get_num_threads(), min(16, os.cpu_count() or 1)))
+    P = O.make_params(cfg, param_value)
+    ref_loss, grads = O.train_step(P, None, None, clip.cpu(), mask, cfg)
+    assert abs(loss.item() - float(ref_loss)) < 0.02 * abs(float(ref_loss)), (loss.item(), float(ref_loss))
+    named = dict(model.named_parameters())
+    n = 0
+    for name, g in grads.items():
+        if g is None:
+            continue
+        ours = named[name]._sm_grad.detach().double().cpu().reshape(-1)
+        ref = g.double().reshape(-1)
+        if ref.norm().item() < 1e-6:   # analytically zero (a bias feeding a BatchNorm): rounding noise only
+            continue
+        cos = float(torch.dot(ours, ref) / (ours.norm() * ref.norm() + 1e-30))
+        assert cos > 0.98, (name, cos)
+        assert abs(ours.norm().item() / ref.norm().item() - 1) < 0.10, name
+        n += 1
+    assert n > 150
+
+
 def test_bf16_full_c2_step_properties():
     """The full C2 step (B=256, T=8, 224^2, bf16, dropout/DropPath on, auto resident
     stages) twice: the fused loss equals the reference formula (patchify, unbiased
