@@ -66,6 +66,9 @@ def gemm(args):
         ("dec qkv fwd", B * 6272, 1152, 384), ("s0 expand fwd", B * 8 * 12544, 384, 96),
         ("s0 proj fwd", B * 8 * 12544, 96, 384), ("s2 fc1 fwd", B * 8 * 784, 1536, 384),
         ("dec proj fwd", B * 6272, 384, 384), ("s1 qkv fwd", B * 8 * 3136, 576, 192)]
+    # --mf 32,16: the K loop's MFMA shape A/B (gemm_tuning mf16_min_k: 16 -> every K-major-A
+    # v2 GEMM on 16x16x32, 32 -> none), interleaved rounds in one process
+    mfs = [int(v) for v in args.mf.split(",")] if args.mf else [None]
     for name, M, N, Kd in cases:
         if args.only and args.only not in name:
             continue
@@ -73,13 +76,23 @@ def gemm(args):
         w = torch.randn(N, Kd, device="cuda").to(torch.bfloat16)
         b = torch.randn(N, device="cuda")
         f = 2.0 * M * N * Kd
-        t = timeit(lambda: K.linear(x, w, b), args.iters)
         dy = torch.randn(M, N, device="cuda").to(torch.bfloat16)
-        t_dx = timeit(lambda: K.linear_dx(dy, w), args.iters)
         sink = torch.zeros(N, Kd, device="cuda")
-        t_dw = timeit(lambda: K.linear_dw(dy, x, sink), args.iters)
-        print(f"{name}: M={M} N={N} K={Kd}  fwd {t:7.2f} ms {f / t / 1e9:7.1f} TF/s | dX {t_dx:7.2f} ms "
-              f"{f / t_dx / 1e9:7.1f} | dW {t_dw:7.2f} ms {f / t_dw / 1e9:7.1f}", flush=True)
+        ops = {"fwd": lambda: K.linear(x, w, b), "dX": lambda: K.linear_dx(dy, w),
+               "dW": lambda: K.linear_dw(dy, x, sink)}
+        times = {(mf, o): [] for mf in mfs for o in ops}
+        for _ in range(args.rounds):
+            for mf in mfs:
+                prev = K.gemm_tuning("mf16_min_k", 0 if mf == 16 else 1 << 30) if mf else None
+                for o, fn in ops.items():
+                    times[(mf, o)].append(timeit(fn, args.iters))
+                if mf:
+                    K.gemm_tuning("mf16_min_k", prev)
+        for mf in mfs:
+            med = {o: sorted(times[(mf, o)])[len(times[(mf, o)]) // 2] for o in ops}
+            print(f"{name} [mf {mf or 'default'}]: M={M} N={N} K={Kd}  fwd {med['fwd']:7.3f} ms "
+                  f"{f / med['fwd'] / 1e9:7.1f} TF/s | dX {med['dX']:7.3f} ms {f / med['dX'] / 1e9:7.1f} | "
+                  f"dW {med['dW']:7.3f} ms {f / med['dW'] / 1e9:7.1f}", flush=True)
         del x, w, dy, sink
         torch.cuda.empty_cache()
 
@@ -314,7 +327,8 @@ if __name__ == "__main__":
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--only", default="")
     ap.add_argument("--bwd-shapes", default="", help="attn: MFMA shapes of the backward to A/B, e.g. 32,16")
-    ap.add_argument("--rounds", type=int, default=1, help="attn: interleaved rounds per backward shape")
+    ap.add_argument("--rounds", type=int, default=1, help="attn / gemm: interleaved rounds per variant")
+    ap.add_argument("--mf", default="", help="gemm: K-loop MFMA shapes to A/B, e.g. 32,16")
     a = ap.parse_args()
     from ssl_mae_amd.build import build
     build()

@@ -1,10 +1,13 @@
 # HBM traffic of the bench's roofline kernel from PMC counters (MI355X_MICROARCH.md, HBM
 # section): FETCH_SIZE and WRITE_SIZE in separate passes (they cannot share a pass),
 # FETCH_SIZE doubled for 16-B streaming reads on gfx950.  Writes
-# profiles/<TAG>_traffic.json, which bench.py folds into roofline.traffic.
+# gpurun_out/<TAG>_traffic.json (copied to profiles/, where bench.py folds it into
+# roofline.traffic).  KERNELS: '+'-joined kernel names, default the decoder attention
+# backward pair on v_mfma_f32_16x16x32_bf16 (the bench's default probe).
 set -e
 TAG=${1:-r01}
+KERNELS=${2:-"attn_bwd_dq16_bf16<64, true, 4>+attn_bwd_dkdv16_bf16<64, true, 4>"}
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 1 --warmup 1 > gpurun_out/pmc_fetch.log 2>&1
-timeout -k 10 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 1 --warmup 1 > gpurun_out/pmc_write.log 2>&1
-python scripts/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write "attn_fwd_bf16<64, true>" gpurun_out/${TAG}_traffic.json
+timeout -k 10 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --no-cpu-baseline --no-calibration --steps 1 --warmup 1 > gpurun_out/pmc_fetch.log 2>&1
+timeout -k 10 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --no-cpu-baseline --no-calibration --steps 1 --warmup 1 > gpurun_out/pmc_write.log 2>&1
+python scripts/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write "$KERNELS" gpurun_out/${TAG}_traffic.json

@@ -561,9 +561,14 @@ constexpr uint32_t BUF_OOB = 0x40000000u;   // >= num_records: the load returns 
 constexpr int XA_MAXK = 1536;                // IMP 6: channels of the transformed A operand
 constexpr int XB_MAXK = 256;                 // IMP 11 / 12: channels of the BatchNorm-input A operand
 
+// [64][ROWS] MN-major tile (ROWS*2-B rows), 16-B chunks XOR-swizzled by k-row bits 0-1 and 3:
+// the transposed fragment reads of both MFMA shapes are bank-conflict free (32x32x16: k-rows
+// 8h + 0..3 x 32 columns per half-wave; 16x16x32: k-rows {0..3, 8..11} x 16 columns) and so
+// are the 8-lane 16-B stores (simulated: every read / write pattern at ROWS 64 / 128 / 256).
+// The key is invariant under the loaders' k-row step (a multiple of 16).
 template <int ROWS>
-SM_DEV int mnmaj_off_r(int krow, int col) {   // [64][ROWS] MN-major tile (ROWS*2-B rows)
-  return krow * (ROWS * 2) + ((((col >> 3) ^ ((krow & 3) << 2))) << 4) + ((col & 7) << 1);
+SM_DEV int mnmaj_off_r(int krow, int col) {
+  return krow * (ROWS * 2) + (((col >> 3) ^ ((krow & 3) << 2) ^ (((krow >> 3) & 1) << 1)) << 4) + ((col & 7) << 1);
 }
 
 template <int ROWS, int NT, bool KMAJ>
@@ -628,6 +633,87 @@ SM_DEV bf16x8 lread_frag_r(const char* lds, int rb, int s, int l = threadIdx.x &
     s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     return __builtin_bit_cast(bf16x8, v);
   }
+}
+
+// v_mfma_f32_16x16x32_bf16 fragment of the 16-row (or column) block rb, 32-deep K substep s:
+// lane l holds row rb + (l & 15), k = 32 s + 8 (l >> 4) + 0..7 (the same map for both operands)
+template <bool KMAJ, int ROWS>
+SM_DEV bf16x8 lread_frag16(const char* lds, int rb, int s, int l = threadIdx.x & 63) {
+  if (KMAJ) {
+    return *(const bf16x8*)(lds + kmaj_off(rb + (l & 15), 4 * s + (l >> 4)));
+  } else {
+    // each 16-lane group reads k-rows 32 s + 8 g + 0..3 (then + 4..7) x 16 columns; the
+    // transposing read hands lane i of the group column rb + i of those 4 rows
+    const int g = l >> 4, i = l & 15, q = i >> 2, p = i & 3;
+    const int col = rb + 4 * p, k0 = 32 * s + 8 * g + q;
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + mnmaj_off_r<ROWS>(k0, col)));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + mnmaj_off_r<ROWS>(k0 + 4, col)));
+    typedef __attribute__((ext_vector_type(8))) short s16x8;
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+// A wave's 64 x 64 (or 64 x 32) tile on v_mfma_f32_16x16x32_bf16.  The accumulators keep the
+// 32x32x16 storage (f32x16 per 32 x 32 block) so the epilogues are shared: during the K loop
+// block (i, j) holds its four 16 x 16 sub-blocks q = 2a + b (a: row half, b: column half) in
+// elements 4q .. 4q + 3, each in the 16x16 output map (operands swapped as in the 32x32 loop:
+// lane l has tile row 16a + (l & 15), columns 16b + 4 (l >> 4) + 0..3).  acc16_to_32 then
+// moves them into the 32x32 map (row l & 31, columns (r & 3) + 8 (r >> 2) + 4 (l >> 5)):
+// per column half b and element e, v_permlane16_swap(X, Y) of the a = 0 / a = 1 values gives
+// {X0 Y0 X2 Y2} / {X1 Y1 X3 Y3} (16-lane rows), and v_permlane32_swap of those
+// {X0 Y0 X1 Y1} = element 8b + e and {X2 Y2 X3 Y3} = element 8b + 4 + e.
+// one 16-column B fragment (column block j of the wave tile) against the four A fragments
+// (the B fragments are read one at a time: 20 live fragment registers instead of 32)
+template <int NJ>
+SM_DEV __attribute__((always_inline)) void mma16_col(f32x16 (&acc)[2][NJ], const bf16x8 (&af)[4], bf16x8 bj,
+                                                      int j) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = 2 * (i & 1) + (j & 1);
+    f32x16& v = acc[i >> 1][j >> 1];
+    f32x4 c = {v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bj, af[i], c, 0, 0, 0);
+    v[4 * q] = c[0];
+    v[4 * q + 1] = c[1];
+    v[4 * q + 2] = c[2];
+    v[4 * q + 3] = c[3];
+  }
+}
+// issue order of a substep: the A fragments and B fragments 0 and 1, then per column block j
+// its four MFMAs with B fragment j + 2 read in front of them (one B fragment in flight behind
+// the MFMAs instead of a full wait per block; 24 live fragment registers)
+template <bool AK, bool BK, int NB>
+SM_DEV __attribute__((always_inline)) void mma16_schedule() {
+  constexpr int RA = AK ? 1 : 2, RB = BK ? 1 : 2;   // LDS read instructions per fragment
+  __builtin_amdgcn_sched_group_barrier(0x100, 4 * RA + 2 * RB, 0);
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    if (j + 2 < NB) __builtin_amdgcn_sched_group_barrier(0x100, RB, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+  }
+}
+template <int NJ>
+SM_DEV __attribute__((always_inline)) void acc16_to_32(f32x16 (&acc)[2][NJ]) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {   // elements {e, 4 + e, 8 + e, 12 + e} in, the same four out
+        f32x16& v = acc[i][j];
+        const auto x0 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[e]), __float_as_uint(v[8 + e]), false, false);
+        const auto x1 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[4 + e]), __float_as_uint(v[12 + e]), false,
+                                                         false);
+        const auto y0 = __builtin_amdgcn_permlane32_swap(x0[0], x0[1], false, false);
+        const auto y1 = __builtin_amdgcn_permlane32_swap(x1[0], x1[1], false, false);
+        v[e] = __uint_as_float(y0[0]);
+        v[4 + e] = __uint_as_float(y0[1]);
+        v[8 + e] = __uint_as_float(y1[0]);
+        v[12 + e] = __uint_as_float(y1[1]);
+      }
+    }
 }
 
 // ------------------------------------------------------------ implicit im2col loaders
@@ -837,9 +923,12 @@ struct XformColsB {
 // SIMD -- scratch spills inside the K loop -- so it runs at 2 waves / SIMD.)
 // BNV: block columns, 128 (waves 64 wide) or 64 (waves 32 wide: narrow outputs such as the
 // stem conv's 48-channel data gradient, where a 128-column tile computed 62.5 % padding).
-template <bool AK, bool BK, typename TC, bool VEC, int BMV, int IMP = 0, int BNV = 128>
+// MF: MFMA shape of the K loop, 32 (v_mfma_f32_32x32x16_bf16) or 16 (v_mfma_f32_16x16x32_bf16,
+// mma16_col; same operand images and epilogue)
+template <bool AK, bool BK, typename TC, bool VEC, int BMV, int IMP = 0, int BNV = 128, int MF = 32>
 __global__ __launch_bounds__(BMV * 2, (BMV == 256 && IMP != 5 && IMP != 6 && IMP != 7) ? 4 : 2) void gemm_bf16_v2(GemmArgs g) {
   constexpr int NT = BMV * 2, NJ = BNV / 64;
+  static_assert(MF == 32 || (MF == 16 && IMP == 0), "16x16x32 K loop: plain operands only");
   static_assert(BNV == 128 || (BNV == 64 && IMP != 8 && IMP != 9 && IMP != 10 && IMP != 11),
                 "64-column tiles: no statistics / side-output epilogue");
   constexpr bool XB = IMP == 5 || IMP == 7;
@@ -992,21 +1081,34 @@ __global__ __launch_bounds__(BMV * 2, (BMV == 256 && IMP != 5 && IMP != 6 && IMP
       load_a(k0 + BKT, ra);
       load_b(k0 + BKT, rb);
     }
+    if constexpr (MF == 16) {
 #pragma unroll
-    for (int s = 0; s < BKT / 16; ++s) {
-      bf16x8 af[2], bfr[NJ];
+      for (int s = 0; s < BKT / 32; ++s) {
+        bf16x8 af[4];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = lread_frag_r<AK, BMV>(la, wm + 32 * i, s);
+        for (int i = 0; i < 4; ++i) af[i] = lread_frag16<AK, BMV>(la, wm + 16 * i, s);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) bfr[j] = lread_frag_r<BK, BNV>(lb, wn + 32 * j, s);
+        for (int j = 0; j < 2 * NJ; ++j) mma16_col<NJ>(acc, af, lread_frag16<BK, BNV>(lb, wn + 16 * j, s), j);
+        mma16_schedule<AK, BK, 2 * NJ>();
+      }
+    } else {
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int s = 0; s < BKT / 16; ++s) {
+        bf16x8 af[2], bfr[NJ];
 #pragma unroll
-        for (int j = 0; j < NJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+        for (int i = 0; i < 2; ++i) af[i] = lread_frag_r<AK, BMV>(la, wm + 32 * i, s);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) bfr[j] = lread_frag_r<BK, BNV>(lb, wn + 32 * j, s);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      }
     }
     __syncthreads();
   }
+  if constexpr (MF == 16) acc16_to_32<NJ>(acc);
   if (csum) {   // block-uniform: reduce the NT / (BMV / 8) threads that share 8 rows
     constexpr int G = BMV / 8;
     float* red = (float*)lds;
@@ -1596,9 +1698,10 @@ int choose_splits(int M, int N, int K, bool bf16) {
 // Tuning knobs (A/B measurement runs only; scripts/ set them through sm_gemm_tuning, the
 // product path never changes them).  Defaults are the measured best per shape family.
 enum { TUNE_VARIANT = 0, TUNE_PP = 1, TUNE_PP_MINN = 2, TUNE_PP_MAXK = 3, TUNE_PP_ROUNDS = 4,
-       TUNE_PP_ROUNDS_SMALLK = 5, TUNE_PP_ROUNDS_MIDK = 6, TUNE_COUNT = 7 };
-constexpr int kTuneDefault[TUNE_COUNT] = {0, 1, 512, 6 * BKT, -1, 8, 2};
-int g_tune[TUNE_COUNT] = {0, 1, 512, 6 * BKT, -1, 8, 2};
+       TUNE_PP_ROUNDS_SMALLK = 5, TUNE_PP_ROUNDS_MIDK = 6, TUNE_MF16_MINK = 7, TUNE_COUNT = 8 };
+constexpr int kMF16Off = 1 << 30;
+constexpr int kTuneDefault[TUNE_COUNT] = {0, 1, 512, 6 * BKT, -1, 8, 2, kMF16Off};
+int g_tune[TUNE_COUNT] = {0, 1, 512, 6 * BKT, -1, 8, 2, kMF16Off};
 int gemm_variant(int M, int N, int K) {
   const int forced = (g_tune[TUNE_VARIANT] >= 1 && g_tune[TUNE_VARIANT] <= 3) ? g_tune[TUNE_VARIANT] : 0;
   if (forced) return forced;
@@ -1635,6 +1738,11 @@ int pp_rounds(const GemmArgs& g) {
   const int forced = g_tune[TUNE_PP_ROUNDS];   // A/B runs; 0 = fully persistent
   return forced >= 0 ? forced : g.K <= 2 * BKT ? g_tune[TUNE_PP_ROUNDS_SMALLK] : g_tune[TUNE_PP_ROUNDS_MIDK];
 }
+// K loop on v_mfma_f32_16x16x32_bf16 (v2's MF = 16) for the BM = 256 plain-operand tiles with
+// a K-major A whose K per block is at least g_tune[TUNE_MF16_MINK].  (With an M/N-major A -- the
+// weight gradients -- and in gemm_bf16_pp the 16x16x32 loop's four A fragments spill 11-36
+// VGPRs at the 128-register cap of two 8-wave blocks per CU: not built.)
+bool mf16_ok(const GemmArgs& g) { return (g.k_chunk < g.K ? g.k_chunk : g.K) >= g_tune[TUNE_MF16_MINK]; }
 template <bool BK, int IMP>
 bool launch_pp(const GemmArgs& g, hipStream_t st) {
   static int slots = 0;   // resident blocks on the device, a multiple of 8 (occupancy query, cached)
@@ -1678,6 +1786,8 @@ void launch_bf16(const GemmArgs& g, int splits, hipStream_t st) {
     }
   }
   if (v == 1) hipLaunchKernelGGL((gemm_bf16_kernel<AK, BK, TC, VEC>), dim3(tiles, 1, splits), dim3(256), 0, st, g);
+  else if (AK && v == 2 && mf16_ok(g))
+    hipLaunchKernelGGL((gemm_bf16_v2<AK, BK, TC, VEC, 256, 0, 128, AK ? 16 : 32>), dim3(tiles * splits), dim3(512), 0, st, g);
   else if (v == 2) hipLaunchKernelGGL((gemm_bf16_v2<AK, BK, TC, VEC, 256>), dim3(tiles * splits), dim3(512), 0, st, g);
   else hipLaunchKernelGGL((gemm_bf16_v2<AK, BK, TC, VEC, 128>), dim3(tiles * splits), dim3(256), 0, st, g);
 }

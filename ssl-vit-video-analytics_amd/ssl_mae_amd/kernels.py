@@ -45,7 +45,8 @@ def gemm_persistent(mode=-1):
     return int(query("sm_gemm_persistent", int(mode)))
 
 
-GEMM_TUNING_KEYS = ("variant", "pp", "pp_min_n", "pp_max_k", "pp_rounds", "pp_rounds_small_k", "pp_rounds_mid_k")
+GEMM_TUNING_KEYS = ("variant", "pp", "pp_min_n", "pp_max_k", "pp_rounds", "pp_rounds_small_k", "pp_rounds_mid_k",
+                    "mf16_min_k")
 
 
 def gemm_tuning(key, value=None, reset=False):
