@@ -62,7 +62,7 @@ def gemm_tuning(key, value=None, reset=False):
 
 
 _GEMM_TUNING_DEFAULTS = {"variant": 0, "pp": 1, "pp_min_n": 512, "pp_max_k": 384, "pp_rounds": -1,
-                         "pp_rounds_small_k": 8, "pp_rounds_mid_k": 2}
+                         "pp_rounds_small_k": 8, "pp_rounds_mid_k": 2, "mf16_min_k": 1 << 30}
 
 
 def gemm_tuning_nondefault():
