@@ -96,9 +96,9 @@ def main():
         tot = {}
         for r in csv.DictReader(open(csvf)):
             nm = r["Name"]
-            for key, pat in (("attention decoder bwd", r"attn_bwd_(dq|dkdv)_bf16<64"),
+            for key, pat in (("attention decoder bwd", r"attn_bwd_(dq|dkdv)(16)?_bf16<64"),
                              ("attention decoder fwd", r"attn_fwd_bf16<64"),
-                             ("attention encoder bwd (both L)", r"attn_bwd_(dq|dkdv)_bf16<32"),
+                             ("attention encoder bwd (both L)", r"attn_bwd_(dq|dkdv)(16)?_bf16<32"),
                              ("attention encoder fwd (both L)", r"attn_fwd_bf16<32")):
                 if re.search(pat, nm):
                     tot[key] = tot.get(key, 0.0) + float(r["TotalDurationNs"]) / 1e6 / steps
