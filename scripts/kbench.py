@@ -156,6 +156,36 @@ def dwx(args):
         torch.cuda.empty_cache()
 
 
+def dxgelu(args):
+    """fc2 data gradient through dropout(GELU(pre)) with the h side output (linear_dx_gelu):
+    persistent form (gemm_bf16_pp IMP 9) against one tile per block (v2), interleaved rounds;
+    outputs compared bitwise."""
+    B = args.batch
+    dev = "cuda"
+    for name, M, N, H, p in [("dec fc2", B * 6272, 384, 1536, 0.1), ("s2 fc2", B * 8 * 784, 384, 1536, 0.0),
+                             ("s1 fc2", B * 8 * 3136, 192, 768, 0.0)]:
+        if args.only and args.only not in name:
+            continue
+        pre = torch.randn(M, H, device=dev).to(torch.bfloat16)
+        dy = (torch.randn(M, N, device=dev) * 0.1).to(torch.bfloat16)
+        w = (torch.randn(N, H, device=dev) * 0.05).to(torch.bfloat16)
+        out = {}
+        times = {0: [], 1: []}
+        for _ in range(args.rounds):
+            for pp in (0, 1):
+                prev = K.gemm_persistent(pp)
+                times[pp].append(timeit(lambda: K.linear_dx_gelu(dy, w, pre, p, 77), args.iters))
+                out[pp] = K.linear_dx_gelu(dy, w, pre, p, 77)
+                K.gemm_persistent(prev)
+        same = torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+        med = {k: sorted(v)[len(v) // 2] for k, v in times.items()}
+        gb = (M * N + 3 * M * H) * 2 / 1e9
+        print(f"{name}: M={M} N={N} H={H} p={p}  v2 {med[0]:7.3f} ms | persistent {med[1]:7.3f} ms "
+              f"({gb / med[1]:5.2f} TB/s algorithmic) | bit-identical {same}", flush=True)
+        del pre, dy, w, out
+        torch.cuda.empty_cache()
+
+
 def dwse(args):
     """MBConv projection weight gradient over the SE output: se_scale + linear_dw against
     linear_dw_se (h3 formed in the GEMM's operand loads); outputs compared bitwise."""
@@ -321,7 +351,7 @@ def mbconv(args):
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("what", choices=["attn", "gemm", "gemmk", "mbconv", "dw", "dwx", "dwse", "stem", "gemmw",
-                                     "bnstats"])
+                                     "bnstats", "dxgelu"])
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--drop", type=float, default=0.1)
     ap.add_argument("--iters", type=int, default=5)
@@ -333,4 +363,4 @@ if __name__ == "__main__":
     from ssl_mae_amd.build import build
     build()
     {"attn": attn, "gemm": gemm, "gemmk": gemmk, "mbconv": mbconv, "dw": dw, "dwx": dwx, "dwse": dwse, "stem": stem, "gemmw": gemmw,
-     "bnstats": bnstats}[a.what](a)
+     "bnstats": bnstats, "dxgelu": dxgelu}[a.what](a)

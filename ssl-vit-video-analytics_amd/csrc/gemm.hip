@@ -1329,6 +1329,84 @@ SM_DEV __attribute__((always_inline)) void pp_stage_runs(const f32x16 (&acc)[2][
   }
 }
 
+// GELU backward with the activation side output (fc2 data gradient, sm_linear_dx_gelu: v2's IMP 9
+// epilogue): each 32-row image first receives the saved pre-activation as whole 128-B lines (8 rows
+// per 16-B buffer load, rows / columns past M / N read zero), every lane reads its own four runs
+// back, leaves dx = drop(v GELU'(pre)) in the accumulators in run order and writes
+// h = bf16(drop(GELU(pre))) over the run it read.  The images then go to g.aux_out, pp_stage_runs
+// stages dx for C -- gemm_epilogue's values and roundings (AUXS path), so bit-identical.  No bias /
+// residual / row scale (the launch checks).
+SM_DEV __attribute__((always_inline)) void pp_stage_gelu_bwd(const GemmArgs& g, f32x16 (&acc)[2][2], int m0, int n0,
+                                                             int wm, int wn, int l, char* img) {
+  const int h = l >> 5, c = l & 7;
+  const uint32_t s32 = seed32(g.seed), thr = drop_thr(g.drop_p);
+  const float ks = g.drop_p > 0.f ? drop_scale(g.drop_p) : 1.f;
+  const int colq = n0 + wn + 8 * c;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r0 = m0 + wm + 32 * i;
+    const auto prs = rows_rsrc((const __bf16*)g.aux + (int64_t)r0 * g.ldc, (int64_t)g.M - r0, g.ldc * 2);
+    uint4 av[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = (l >> 3) + 8 * q;
+      av[q] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            prs, colq < g.N ? (uint32_t)((r * g.ldc + colq) * 2) : BUF_OOB, 0, 0));
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = (l >> 3) + 8 * q;
+      *(uint4*)(img + i * 4096 + r * 128 + ((c ^ rs_swz(r)) << 4)) = av[q];
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the lines other lanes staged
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const RowStage rs_{img + i * 4096};
+    const int row = m0 + wm + 32 * i + (l & 31);
+    const uint32_t rb = drop_rowbase(s32, (uint64_t)row);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int col = n0 + wn + 32 * j + 16 * p + 8 * h;
+        const int rr_ = l & 31, ch_ = 4 * j + 2 * p + h;
+        float pre[8];
+        load8((const __bf16*)(img + i * 4096 + rr_ * 128 + ((ch_ ^ rs_swz(rr_)) << 4)), pre);
+        float v[8], hg[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[i][j][8 * p + e]),
+                                                           __float_as_uint(acc[i][j][8 * p + 4 + e]), false, false);
+          v[e] = __uint_as_float(sw[0]);
+          v[4 + e] = __uint_as_float(sw[1]);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          v[e] = fmaf(v[e], g.alpha, 0.f);
+          if (g.epi & 2) v[e] = (float)(__bf16)v[e];
+          v[e] *= gelu_grad(pre[e]);
+          hg[e] = gelu_f(pre[e]);
+        }
+        if (g.drop_p > 0.f) {
+#pragma unroll
+          for (int e4 = 0; e4 < 8; e4 += 4) {
+            const uint32_t hv = drop_hash(rb, (uint32_t)(col + e4));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float m = ((hv >> (8 * e)) & 0xFFu) >= thr ? ks : 0.f;
+              v[e4 + e] *= m;
+              hg[e4 + e] *= m;
+            }
+          }
+        }
+        stage_put<__bf16>(rs_, 0, j, p, h, l, hg);   // over this lane's own pre run
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[i][j][8 * p + e] = v[e];
+      }
+  }
+}
+
 // The wave's two images -> C by unconditional buffer stores (RowStage::flush's order and
 // statistics); rows past M are dropped by the descriptor, columns past N by the offset.
 template <bool STATS>
@@ -1374,14 +1452,16 @@ SM_DEV __attribute__((always_inline)) void pp_flush(const GemmArgs& g, const voi
 // K-major A; B K-major (forward, y = x W^T) or M/N-major (data gradient, dX = dy W); bf16
 // output; IMP 0 plain / 8 output BatchNorm statistics / 11, 12 BatchNorm-input A operand with /
 // without the statistics (v2's IMP 11 / 12 transform in put()) / 13 GELU with the
-// pre-activation side output (pp_stage_gelu_aux).  No split-K (k_begin = 0, k_chunk >=
+// pre-activation side output (pp_stage_gelu_aux) / 9 GELU backward with the activation side
+// output (pp_stage_gelu_bwd).  No split-K (k_begin = 0, k_chunk >=
 // K).  Grid: a multiple of 8 blocks, at most T / 8 per XCD group; block b serves group b & 7
 // (its tiles are a contiguous m-major range, so concurrently running blocks share A panels in
 // the XCD's L2) and walks tiles b >> 3, + gridDim.x / 8, ... of it.
 template <bool BK, int IMP>
 __global__ __launch_bounds__(512, 4) void gemm_bf16_pp(GemmArgs g) {
-  static_assert(IMP == 0 || IMP == 8 || IMP == 11 || IMP == 12 || IMP == 13,
-                "persistent form: plain, statistics, BatchNorm-input (+ statistics) or GELU + pre epilogue");
+  static_assert(IMP == 0 || IMP == 8 || IMP == 9 || IMP == 11 || IMP == 12 || IMP == 13,
+                "persistent form: plain, statistics, GELU backward + activation, BatchNorm-input (+ statistics) "
+                "or GELU + pre epilogue");
   constexpr bool STATS = IMP == 8 || IMP == 11;
   constexpr bool XA = IMP == 11 || IMP == 12;   // A = bf16(a sc + sh) formed on its way to LDS (as v2)
   __shared__ float xtab[XA ? 2 * XB_MAXK : 4];
@@ -1533,11 +1613,12 @@ __global__ __launch_bounds__(512, 4) void gemm_bf16_pp(GemmArgs g) {
   int cm0 = lm0, cn0 = ln0;
   for (int in = it + qstep; in < cnt; in += qstep) {
     if constexpr (IMP == 13) pp_stage_gelu_aux(g, acc, cm0, cn0, wm, wn, opaque_tid() & 63, img);
+    else if constexpr (IMP == 9) pp_stage_gelu_bwd(g, acc, cm0, cn0, wm, wn, opaque_tid() & 63, img);
     else pp_stage(g, acc, cm0, cn0, wm, wn, opaque_tid() & 63, img);
     setup(in);
     issue(0);
-    if constexpr (IMP == 13) {   // pre -> aux (stores younger than the next operands), then y
-      pp_flush<false>(g, g.aux, cm0, cn0, wm, wn, opaque_tid() & 63, img);
+    if constexpr (IMP == 13 || IMP == 9) {   // pre -> aux / h -> aux_out (stores younger than the next operands), then C
+      pp_flush<false>(g, IMP == 13 ? g.aux : g.aux_out, cm0, cn0, wm, wn, opaque_tid() & 63, img);
       pp_stage_runs(acc, opaque_tid() & 63, img);
     }
     pp_flush<STATS>(g, g.C, cm0, cn0, wm, wn, opaque_tid() & 63, img);
@@ -1549,6 +1630,10 @@ __global__ __launch_bounds__(512, 4) void gemm_bf16_pp(GemmArgs g) {
   if constexpr (IMP == 13) {
     pp_stage_gelu_aux(g, acc, cm0, cn0, wm, wn, threadIdx.x & 63, img);
     pp_flush<false>(g, g.aux, cm0, cn0, wm, wn, threadIdx.x & 63, img);
+    pp_stage_runs(acc, threadIdx.x & 63, img);
+  } else if constexpr (IMP == 9) {
+    pp_stage_gelu_bwd(g, acc, cm0, cn0, wm, wn, threadIdx.x & 63, img);
+    pp_flush<false>(g, g.aux_out, cm0, cn0, wm, wn, threadIdx.x & 63, img);
     pp_stage_runs(acc, threadIdx.x & 63, img);
   } else {
     pp_stage(g, acc, cm0, cn0, wm, wn, threadIdx.x & 63, img);
@@ -1733,6 +1818,13 @@ bool pp_ok(const GemmArgs& g) {
          (!((g.epi & 1) && g.aux) || (g.beta == 0.f && g.row_scale == nullptr)) && g.aux_out == nullptr &&
          g.K > 0 && g.k_begin == 0 && g.k_chunk >= g.K &&
          (g.K <= 2 * BKT || (g.K <= g_tune[TUNE_PP_MAXK] && g.N >= g_tune[TUNE_PP_MINN]));
+}
+// the GELU-backward data gradient with the activation side output (IMP 9) in the persistent
+// form: the same shape rule, no bias / residual / row scale in its epilogue
+bool pp_ok_gelu_bwd(const GemmArgs& g) {
+  return pp_enabled() && g.partial == nullptr && g.colsum == nullptr && !g.ctrans && g.epi == 4 && g.aux &&
+         g.aux_out && g.bias == nullptr && g.beta == 0.f && g.row_scale == nullptr && g.K > 0 && g.k_begin == 0 &&
+         g.k_chunk >= g.K && (g.K <= 2 * BKT || (g.K <= g_tune[TUNE_PP_MAXK] && g.N >= g_tune[TUNE_PP_MINN]));
 }
 int pp_rounds(const GemmArgs& g) {
   const int forced = g_tune[TUNE_PP_ROUNDS];   // A/B runs; 0 = fully persistent
@@ -2007,6 +2099,10 @@ extern "C" int sm_linear_dx_gelu(int M, int N, int K, const void* dy, const void
   g.drop_p = drop_p; g.seed = seed; g.rows_per_group = 1; g.k_begin = 0; g.k_chunk = N;
   const int v = gemm_variant(g.M, g.N, g.K);
   const int tiles = ((g.N + 127) / 128) * ((g.M + variant_bm(v) - 1) / variant_bm(v));
+  if (v == 2 && pp_ok_gelu_bwd(g) && launch_pp<false, 9>(g, stream)) {
+    SM_CHECK_LAUNCH();
+    return 0;
+  }
   if (v == 2) hipLaunchKernelGGL((gemm_bf16_v2<true, false, __bf16, true, 256, 9>), dim3(tiles), dim3(512), 0, stream, g);
   else hipLaunchKernelGGL((gemm_bf16_v2<true, false, __bf16, true, 128, 9>), dim3(tiles), dim3(256), 0, stream, g);
   SM_CHECK_LAUNCH();

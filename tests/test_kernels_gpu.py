@@ -850,22 +850,23 @@ def test_linear_dw_se_operand(Fr, HW, N, C, acc):
 
 @pytest.mark.parametrize("case", ["bias", "bias_unaligned", "gelu", "branch", "dx", "dx_res", "k128", "k40",
                                   "stats", "k384", "k384_branch", "dx_k384", "stats_k192", "gelu_aux",
-                                  "gelu_aux_k384"])
+                                  "gelu_aux_k384", "gelu_bwd", "gelu_bwd_k384"])
 def test_gemm_persistent_bit_identical(case):
     """The persistent GEMM form (gemm_bf16_pp: tile epilogues written through LDS and stored
     under the next tile's K loop; K <= 128 at 8 tiles per block, K <= 384 with N >= 512 at 2)
     against the one-tile-per-block v2 form, bit for bit: ragged M (a partial last m-tile) and
     N (392 / 520: a partial n-tile), K tails (96, 40: one K-step; 384, 192: several), every
     epilogue option of the plain form (bias, GELU without / with its pre-activation side output,
-    the autocast-rounded branch + dropout + DropPath + residual), the data-gradient layout (M/N-major B), and the
-    BatchNorm-statistics epilogue.  > 512 tiles: the persistent path."""
+    the autocast-rounded branch + dropout + DropPath + residual), the data-gradient layout (M/N-major B), the
+    BatchNorm-statistics epilogue, and the GELU-backward data gradient with its activation side output
+    (sm_linear_dx_gelu, with / without dropout).  > 512 tiles: the persistent path."""
     kk = KK()
     M, N, Kd = 256 * 200 + 77, 392, 96
     if case == "k128":
         Kd = 128
     elif case == "k40":
         Kd = 40
-    elif case in ("k384", "k384_branch", "dx_k384", "gelu_aux_k384"):
+    elif case in ("k384", "k384_branch", "dx_k384", "gelu_aux_k384", "gelu_bwd_k384"):
         N, Kd = 520, 384
     elif case == "stats":
         M, N = 256 * 300 + 13, 384
@@ -888,6 +889,10 @@ def test_gemm_persistent_bit_identical(case):
             rm, rv = torch.zeros(N, device=DEV), torch.ones(N, device=DEV)
             nb = torch.zeros((), dtype=torch.int64, device=DEV)
             return kk.linear_bn_stats(x, w, rm, rv, 0.1, 1e-5, 1, nb) + (rm, rv)
+        if case in ("gelu_bwd", "gelu_bwd_k384"):   # fc2 dX through dropout(GELU(pre)) + h = dropout(GELU(pre))
+            wt = rnd(Kd, 520, dtype=torch.bfloat16, seed=317, scale=0.2).to(DEV)
+            pre = rnd(M, 520, dtype=torch.bfloat16, seed=318).to(DEV)
+            return kk.linear_dx_gelu(x, wt, pre, 0.1 if case == "gelu_bwd" else 0.0, 79)
         if case in ("gelu_aux", "gelu_aux_k384"):   # fc1: GELU + the pre-activation side output
             drop = 0.1 if case == "gelu_aux" else 0.0
             return kk.linear(x, w, bias, gelu=True, round_branch=True, drop_p=drop, seed=78)
