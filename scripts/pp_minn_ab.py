@@ -1,0 +1,59 @@
+"""Persistent GEMM form below its N >= 512 rule: the stage-1 / stage-2 Linear shapes with
+N = 192 / 384 / 576 (K <= 384), pp_min_n 512 (default) vs 128, interleaved rounds in one
+process; outputs compared bitwise (the persistent form is bit-identical to v2).
+
+    python scripts/pp_minn_ab.py [--rounds 5] [--iters 3]
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "ssl-vit-video-analytics_amd")]
+
+import torch  # noqa: E402
+
+from ssl_mae_amd import kernels as K  # noqa: E402
+from kbench import timeit  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256)
+    a = ap.parse_args()
+    B = a.batch
+    dev = "cuda"
+    M1, M2 = B * 8 * 3136, B * 8 * 784
+    # (name, kind, M, N_out, K_red)
+    cases = [("s1 proj fwd", "fwd", M1, 192, 192), ("s1 qkv fwd", "fwd", M1, 576, 192),
+             ("s1 proj dX", "dx", M1, 192, 192), ("s1 qkv dX", "dx", M1, 192, 576),
+             ("s2/dec proj fwd", "fwd", M2, 384, 384), ("s2/dec proj dX", "dx", M2, 384, 384)]
+    for name, kind, M, N, Kd in cases:
+        x = torch.randn(M, Kd, device=dev).to(torch.bfloat16)
+        if kind == "fwd":
+            w = (torch.randn(N, Kd, device=dev) * 0.05).to(torch.bfloat16)
+            b = torch.randn(N, device=dev)
+            fn = lambda: K.linear(x, w, b)  # noqa: E731
+        else:   # dx[M][N] = dy[M][Kd] w[Kd][N]
+            w = (torch.randn(Kd, N, device=dev) * 0.05).to(torch.bfloat16)
+            fn = lambda: K.linear_dx(x, w)  # noqa: E731
+        times = {512: [], 128: []}
+        outs = {}
+        for _ in range(a.rounds):
+            for mn in (512, 128):
+                prev = K.gemm_tuning("pp_min_n", mn)
+                times[mn].append(timeit(fn, a.iters))
+                outs[mn] = fn()
+                K.gemm_tuning("pp_min_n", prev)
+        same = torch.equal(outs[512], outs[128])
+        med = {k: sorted(v)[len(v) // 2] for k, v in times.items()}
+        print(f"{name}: M={M} N={N} K={Kd}  v2 rule {med[512]:7.3f} ms | persistent {med[128]:7.3f} ms "
+              f"({(med[128] / med[512] - 1) * 100:+.1f} %) | bit-identical {same}", flush=True)
+        del x, w, outs
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
