@@ -1,5 +1,6 @@
 """Persistent GEMM form below its N >= 512 rule: the stage-1 / stage-2 Linear shapes with
-N = 192 / 384 / 576 (K <= 384), pp_min_n 512 (default) vs 128, interleaved rounds in one
+N = 192 / 384 / 576 (K <= 384), minimum N 512 vs 128 (pp_min_n and pp_min_n_fwd together),
+interleaved rounds in one
 process; outputs compared bitwise (the persistent form is bit-identical to v2).
 
     python scripts/pp_minn_ab.py [--rounds 5] [--iters 3]
@@ -44,9 +45,11 @@ def main():
         for _ in range(a.rounds):
             for mn in (512, 128):
                 prev = K.gemm_tuning("pp_min_n", mn)
+                prev_f = K.gemm_tuning("pp_min_n_fwd", mn)
                 times[mn].append(timeit(fn, a.iters))
                 outs[mn] = fn()
                 K.gemm_tuning("pp_min_n", prev)
+                K.gemm_tuning("pp_min_n_fwd", prev_f)
         same = torch.equal(outs[512], outs[128])
         med = {k: sorted(v)[len(v) // 2] for k, v in times.items()}
         print(f"{name}: M={M} N={N} K={Kd}  v2 rule {med[512]:7.3f} ms | persistent {med[128]:7.3f} ms "
