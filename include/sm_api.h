@@ -51,8 +51,7 @@ int sm_gemm_persistent(int mode);
  * 2 / 3 persistent form's minimum N / maximum K at K > 128, 4 tiles per persistent block
  * (-1 = per-K rule, 0 = fully persistent), 5 / 6 tiles per block at K <= 128 / above,
  * 7 minimum K per block for the v_mfma_f32_16x16x32_bf16 K loop of K-major-A tiles
- * (default 1 << 30 = off: measured neutral), 8 the persistent form's minimum N at K > 128 for
- * a K-major B (forward; key 2 is the data gradient's).
+ * (default 1 << 30 = off: measured neutral).
  * *prev <- the current value; set > 0 stores value, set < 0 restores the default.
  * Returns 0, or -2 for an unknown key.  Host-side only (no launch). */
 int sm_gemm_tuning(int key, int set, int value, int* prev);

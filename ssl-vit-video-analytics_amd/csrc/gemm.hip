@@ -1570,6 +1570,27 @@ __global__ __launch_bounds__(512, 4) void gemm_bf16_pp(GemmArgs g) {
   auto kstep = [&]() {
 #pragma unroll
     for (int s = 0; s < BKT / 16; ++s) {
+      if constexpr (!BK) {
+        // M/N-major B (data gradient): the second B fragment (two transposed reads) is read
+        // behind the first column's MFMAs -- 4 fragment VGPRs fewer at the 128-register cap
+        // (the all-reads-first order spills 4 VGPRs into this loop); same MFMA order per
+        // accumulator, so the outputs are unchanged
+        bf16x8 af[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) af[i] = lread_frag_r<true, BMV>(la, wm + 32 * i, s);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const bf16x8 bj = lread_frag_r<BK, BNV>(lb, wn + 32 * j, s);
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bj, af[i], acc[i][j], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        continue;
+      }
       bf16x8 af[2], bfr[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) af[i] = lread_frag_r<true, BMV>(la, wm + 32 * i, s);
@@ -1783,11 +1804,10 @@ int choose_splits(int M, int N, int K, bool bf16) {
 // Tuning knobs (A/B measurement runs only; scripts/ set them through sm_gemm_tuning, the
 // product path never changes them).  Defaults are the measured best per shape family.
 enum { TUNE_VARIANT = 0, TUNE_PP = 1, TUNE_PP_MINN = 2, TUNE_PP_MAXK = 3, TUNE_PP_ROUNDS = 4,
-       TUNE_PP_ROUNDS_SMALLK = 5, TUNE_PP_ROUNDS_MIDK = 6, TUNE_MF16_MINK = 7, TUNE_PP_MINN_FWD = 8,
-       TUNE_COUNT = 9 };
+       TUNE_PP_ROUNDS_SMALLK = 5, TUNE_PP_ROUNDS_MIDK = 6, TUNE_MF16_MINK = 7, TUNE_COUNT = 8 };
 constexpr int kMF16Off = 1 << 30;
-constexpr int kTuneDefault[TUNE_COUNT] = {0, 1, 512, 6 * BKT, -1, 8, 2, kMF16Off, 0};
-int g_tune[TUNE_COUNT] = {0, 1, 512, 6 * BKT, -1, 8, 2, kMF16Off, 0};
+constexpr int kTuneDefault[TUNE_COUNT] = {0, 1, 128, 6 * BKT, -1, 8, 2, kMF16Off};
+int g_tune[TUNE_COUNT] = {0, 1, 128, 6 * BKT, -1, 8, 2, kMF16Off};
 int gemm_variant(int M, int N, int K) {
   const int forced = (g_tune[TUNE_VARIANT] >= 1 && g_tune[TUNE_VARIANT] <= 3) ? g_tune[TUNE_VARIANT] : 0;
   if (forced) return forced;
@@ -1814,15 +1834,17 @@ bool pp_enabled() { return g_tune[TUNE_PP] != 0; }
 // there is no A panel to share.  Blocks take at most pp_rounds() tiles each (8 at K <= 128, 2
 // above): fully persistent blocks drift apart, so the n-tile blocks that share an A panel no
 // longer stream it through L2 together (K = 384: -1..+1 % persistent against -6 % at 2 tiles).
-// kmajor_b: a forward GEMM (B = W [N][K]).  There the persistent form also pays below N = 512
-// (N = 192 / 384 at K = 192 / 384: -9 / -10 %), where the data gradient's (M/N-major B) loses
-// 8-13 % (profiles/r06y_pp_minn_ab.txt): the minimum N is per layout.
-bool pp_ok(const GemmArgs& g, bool kmajor_b = false) {
-  const int minn = kmajor_b ? g_tune[TUNE_PP_MINN_FWD] : g_tune[TUNE_PP_MINN];
+// Round 6: at K <= 384 the persistent form also pays below N = 512 (the old minimum): forward
+// N = 192 / 384 -9..-11 %, and, once its K loop reads the data gradient's M/N-major B fragments
+// column by column (no spills), the data gradient -1.4..-3.9 % (it lost 6-13 % before); past
+// K = 384 the data gradient still loses 2-4 %, the forward gains 1-2.5 % (not taken;
+// profiles/r06y_pp_minn_ab.txt).  The minimum N is now 128 (two n-tiles: N = 96 keeps one tile
+// per block, see above).
+bool pp_ok(const GemmArgs& g) {
   return pp_enabled() && g.partial == nullptr && g.colsum == nullptr && !g.ctrans && !(g.epi & 4) &&
          (!((g.epi & 1) && g.aux) || (g.beta == 0.f && g.row_scale == nullptr)) && g.aux_out == nullptr &&
          g.K > 0 && g.k_begin == 0 && g.k_chunk >= g.K &&
-         (g.K <= 2 * BKT || (g.K <= g_tune[TUNE_PP_MAXK] && g.N >= minn));
+         (g.K <= 2 * BKT || (g.K <= g_tune[TUNE_PP_MAXK] && g.N >= g_tune[TUNE_PP_MINN]));
 }
 // the GELU-backward data gradient with the activation side output (IMP 9) in the persistent
 // form: the same shape rule, no bias / residual / row scale in its epilogue
@@ -1874,7 +1896,7 @@ void launch_bf16(const GemmArgs& g, int splits, hipStream_t st) {
   const int bm = variant_bm(v), bn = variant_bn(v);
   const int tiles = ((g.N + bn - 1) / bn) * ((g.M + bm - 1) / bm);
   if constexpr (AK && VEC && sizeof(TC) == 2) {
-    if (v == 2 && splits == 1 && pp_ok(g, BK)) {
+    if (v == 2 && splits == 1 && pp_ok(g)) {
       if ((g.epi & 1) && g.aux) {   // fc1: GELU + pre-activation side output
         if (launch_pp<BK, 13>(g, st)) return;
       } else if (launch_pp<BK, 0>(g, st)) {

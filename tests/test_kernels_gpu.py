@@ -850,7 +850,8 @@ def test_linear_dw_se_operand(Fr, HW, N, C, acc):
 
 @pytest.mark.parametrize("case", ["bias", "bias_unaligned", "gelu", "branch", "dx", "dx_res", "k128", "k40",
                                   "stats", "k384", "k384_branch", "dx_k384", "stats_k192", "gelu_aux",
-                                  "gelu_aux_k384", "gelu_bwd", "gelu_bwd_k384", "k384_n264"])
+                                  "gelu_aux_k384", "gelu_bwd", "gelu_bwd_k384", "k384_n264",
+                                  "dx_k384_n264"])
 def test_gemm_persistent_bit_identical(case):
     """The persistent GEMM form (gemm_bf16_pp: tile epilogues written through LDS and stored
     under the next tile's K loop; K <= 128 at 8 tiles per block, K <= 384 with N >= 512 at 2)
@@ -868,7 +869,7 @@ def test_gemm_persistent_bit_identical(case):
         Kd = 40
     elif case in ("k384", "k384_branch", "dx_k384", "gelu_aux_k384", "gelu_bwd_k384"):
         N, Kd = 520, 384
-    elif case == "k384_n264":   # forward below N = 512 (the forward's persistent rule)
+    elif case in ("k384_n264", "dx_k384_n264"):   # K = 384 below N = 512 (persistent since round 6)
         N, Kd = 264, 384
     elif case == "stats":
         M, N = 256 * 300 + 13, 384
@@ -882,7 +883,7 @@ def test_gemm_persistent_bit_identical(case):
     rs = (torch.rand(64, generator=torch.Generator().manual_seed(314)) * 2).to(DEV)
 
     def run():
-        if case in ("dx", "dx_res", "dx_k384"):   # dX[M][Kd'] = dy[M][N] w[N][Kd']: here dy = x, w' = [Kd][N']
+        if case in ("dx", "dx_res", "dx_k384", "dx_k384_n264"):   # dX[M][Kd'] = dy[M][N] w[N][Kd']: here dy = x, w' = [Kd][N']
             n2 = 520 if case == "dx_k384" else 264
             wt = rnd(Kd, n2, dtype=torch.bfloat16, seed=315, scale=0.2).to(DEV)
             r2 = rnd(M, n2, dtype=torch.bfloat16, seed=316).to(DEV) if case == "dx_res" else None
