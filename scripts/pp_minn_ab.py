@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--dx", action="store_true",
                     help="instead: data-gradient shapes, v2 vs persistent at every K (pp_min_n 0, pp_max_k 1536 "
                          "against pp disabled)")
+    ap.add_argument("--arms", default="",
+                    help="JSON list of gemm_tuning dicts to compare instead (first = baseline), e.g. "
+                         "'[{\"pp_rounds_mid_k\": 2}, {\"pp_rounds_mid_k\": 4}]'")
     a = ap.parse_args()
     B = a.batch
     dev = "cuda"
@@ -58,19 +61,27 @@ def main():
             arms = ({"pp": 0}, {"pp": 1, "pp_min_n": 0, "pp_max_k": 1536})
         if a.maxk:
             arms = ({"pp_min_n": 0, "pp_max_k": 384}, {"pp_min_n": 0, "pp_max_k": 1536})
-        times = {0: [], 1: []}
+        if a.arms:
+            import json
+            arms = tuple(json.loads(a.arms))
+        times = {i: [] for i in range(len(arms))}
         outs = {}
         for _ in range(a.rounds):
-            for arm in (0, 1):
+            for arm in range(len(arms)):
                 prev = {k: K.gemm_tuning(k, v) for k, v in arms[arm].items()}
                 times[arm].append(timeit(fn, a.iters))
                 outs[arm] = fn()
                 for k, v in prev.items():
                     K.gemm_tuning(k, v)
-        same = torch.equal(outs[0], outs[1])
+        same = all(torch.equal(outs[0], outs[i]) for i in outs)
         med = {k: sorted(v)[len(v) // 2] for k, v in times.items()}
-        print(f"{name}: M={M} N={N} K={Kd}  v2 rule {med[0]:7.3f} ms | persistent {med[1]:7.3f} ms "
-              f"({(med[1] / med[0] - 1) * 100:+.1f} %) | bit-identical {same}", flush=True)
+        if not a.arms:
+            print(f"{name}: M={M} N={N} K={Kd}  v2 rule {med[0]:7.3f} ms | persistent {med[1]:7.3f} ms "
+                  f"({(med[1] / med[0] - 1) * 100:+.1f} %) | bit-identical {same}", flush=True)
+        else:
+            cols = " | ".join(f"{json.dumps(arms[i])} {med[i]:7.3f} ms ({(med[i] / med[0] - 1) * 100:+.1f} %)"
+                              for i in range(len(arms)))
+            print(f"{name}: M={M} N={N} K={Kd}  {cols} | bit-identical {same}", flush=True)
         del x, w, outs
         torch.cuda.empty_cache()
 
