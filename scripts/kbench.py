@@ -163,7 +163,7 @@ def dxgelu(args):
     B = args.batch
     dev = "cuda"
     for name, M, N, H, p in [("dec fc2", B * 6272, 384, 1536, 0.1), ("s2 fc2", B * 8 * 784, 384, 1536, 0.0),
-                             ("s1 fc2", B * 8 * 3136, 192, 768, 0.0)]:
+                             ("s1 fc2", B * 8 * 3136, 192, 768, 0.0), ("s1 fc2 (no h)", B * 8 * 3136, 192, 768, 0.0)]:
         if args.only and args.only not in name:
             continue
         pre = torch.randn(M, H, device=dev).to(torch.bfloat16)
@@ -174,8 +174,12 @@ def dxgelu(args):
         for _ in range(args.rounds):
             for pp in (0, 1):
                 prev = K.gemm_persistent(pp)
-                times[pp].append(timeit(lambda: K.linear_dx_gelu(dy, w, pre, p, 77), args.iters))
-                out[pp] = K.linear_dx_gelu(dy, w, pre, p, 77)
+                if name.endswith("(no h)"):
+                    times[pp].append(timeit(lambda: K.linear_dx(dy, w, gelu_pre=pre, drop_p=p, seed=77), args.iters))
+                    out[pp] = (K.linear_dx(dy, w, gelu_pre=pre, drop_p=p, seed=77), pre)
+                else:
+                    times[pp].append(timeit(lambda: K.linear_dx_gelu(dy, w, pre, p, 77), args.iters))
+                    out[pp] = K.linear_dx_gelu(dy, w, pre, p, 77)
                 K.gemm_persistent(prev)
         same = torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
         med = {k: sorted(v)[len(v) // 2] for k, v in times.items()}

@@ -1400,7 +1400,7 @@ SM_DEV __attribute__((always_inline)) void pp_stage_gelu_bwd(const GemmArgs& g, 
             }
           }
         }
-        stage_put<__bf16>(rs_, 0, j, p, h, l, hg);   // over this lane's own pre run
+        if (g.aux_out) stage_put<__bf16>(rs_, 0, j, p, h, l, hg);   // over this lane's own pre run
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc[i][j][8 * p + e] = v[e];
       }
@@ -1639,7 +1639,7 @@ __global__ __launch_bounds__(512, 4) void gemm_bf16_pp(GemmArgs g) {
     setup(in);
     issue(0);
     if constexpr (IMP == 13 || IMP == 9) {   // pre -> aux / h -> aux_out (stores younger than the next operands), then C
-      pp_flush<false>(g, IMP == 13 ? g.aux : g.aux_out, cm0, cn0, wm, wn, opaque_tid() & 63, img);
+      if (IMP == 13 || g.aux_out) pp_flush<false>(g, IMP == 13 ? g.aux : g.aux_out, cm0, cn0, wm, wn, opaque_tid() & 63, img);
       pp_stage_runs(acc, opaque_tid() & 63, img);
     }
     pp_flush<STATS>(g, g.C, cm0, cn0, wm, wn, opaque_tid() & 63, img);
@@ -1654,7 +1654,7 @@ __global__ __launch_bounds__(512, 4) void gemm_bf16_pp(GemmArgs g) {
     pp_stage_runs(acc, threadIdx.x & 63, img);
   } else if constexpr (IMP == 9) {
     pp_stage_gelu_bwd(g, acc, cm0, cn0, wm, wn, threadIdx.x & 63, img);
-    pp_flush<false>(g, g.aux_out, cm0, cn0, wm, wn, threadIdx.x & 63, img);
+    if (g.aux_out) pp_flush<false>(g, g.aux_out, cm0, cn0, wm, wn, threadIdx.x & 63, img);
     pp_stage_runs(acc, threadIdx.x & 63, img);
   } else {
     pp_stage(g, acc, cm0, cn0, wm, wn, threadIdx.x & 63, img);
@@ -1846,11 +1846,11 @@ bool pp_ok(const GemmArgs& g) {
          g.K > 0 && g.k_begin == 0 && g.k_chunk >= g.K &&
          (g.K <= 2 * BKT || (g.K <= g_tune[TUNE_PP_MAXK] && g.N >= g_tune[TUNE_PP_MINN]));
 }
-// the GELU-backward data gradient with the activation side output (IMP 9) in the persistent
-// form: the same shape rule, no bias / residual / row scale in its epilogue
+// the GELU-backward data gradient, with or without the activation side output (IMP 9), in the
+// persistent form: the same shape rule, no bias / residual / row scale in its epilogue
 bool pp_ok_gelu_bwd(const GemmArgs& g) {
   return pp_enabled() && g.partial == nullptr && g.colsum == nullptr && !g.ctrans && g.epi == 4 && g.aux &&
-         g.aux_out && g.bias == nullptr && g.beta == 0.f && g.row_scale == nullptr && g.K > 0 && g.k_begin == 0 &&
+         g.bias == nullptr && g.beta == 0.f && g.row_scale == nullptr && g.K > 0 && g.k_begin == 0 &&
          g.k_chunk >= g.K && (g.K <= 2 * BKT || (g.K <= g_tune[TUNE_PP_MAXK] && g.N >= g_tune[TUNE_PP_MINN]));
 }
 int pp_rounds(const GemmArgs& g) {
@@ -2086,6 +2086,10 @@ static int gemm_run(int ab_dtype, int c_dtype, int a_layout, int b_layout, int M
       !((N & 7) || (ldc & 7)) && K > 0) {   // the GELU-backward dX GEMM: IMP 9 epilogue
     const int v = gemm_variant(M, N, K);
     const int tiles = ((N + 127) / 128) * ((M + variant_bm(v) - 1) / variant_bm(v));
+    if (v == 2 && pp_ok_gelu_bwd(g) && launch_pp<false, 9>(g, stream)) {
+      SM_CHECK_LAUNCH();
+      return 0;
+    }
     if (v == 2) hipLaunchKernelGGL((gemm_bf16_v2<true, false, __bf16, true, 256, 9>), dim3(tiles), dim3(512), 0, stream, g);
     else hipLaunchKernelGGL((gemm_bf16_v2<true, false, __bf16, true, 128, 9>), dim3(tiles), dim3(256), 0, stream, g);
     SM_CHECK_LAUNCH();

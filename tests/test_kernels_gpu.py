@@ -851,7 +851,7 @@ def test_linear_dw_se_operand(Fr, HW, N, C, acc):
 @pytest.mark.parametrize("case", ["bias", "bias_unaligned", "gelu", "branch", "dx", "dx_res", "k128", "k40",
                                   "stats", "k384", "k384_branch", "dx_k384", "stats_k192", "gelu_aux",
                                   "gelu_aux_k384", "gelu_bwd", "gelu_bwd_k384", "k384_n264",
-                                  "dx_k384_n264"])
+                                  "dx_k384_n264", "gelu_bwd_noh"])
 def test_gemm_persistent_bit_identical(case):
     """The persistent GEMM form (gemm_bf16_pp: tile epilogues written through LDS and stored
     under the next tile's K loop; K <= 128 at 8 tiles per block, K <= 384 with N >= 512 at 2)
@@ -892,9 +892,11 @@ def test_gemm_persistent_bit_identical(case):
             rm, rv = torch.zeros(N, device=DEV), torch.ones(N, device=DEV)
             nb = torch.zeros((), dtype=torch.int64, device=DEV)
             return kk.linear_bn_stats(x, w, rm, rv, 0.1, 1e-5, 1, nb) + (rm, rv)
-        if case in ("gelu_bwd", "gelu_bwd_k384"):   # fc2 dX through dropout(GELU(pre)) + h = dropout(GELU(pre))
+        if case in ("gelu_bwd", "gelu_bwd_k384", "gelu_bwd_noh"):   # fc2 dX through dropout(GELU(pre)) (+ h)
             wt = rnd(Kd, 520, dtype=torch.bfloat16, seed=317, scale=0.2).to(DEV)
             pre = rnd(M, 520, dtype=torch.bfloat16, seed=318).to(DEV)
+            if case == "gelu_bwd_noh":   # without the side output (sm_gemm's IMP 9 path)
+                return (kk.linear_dx(x, wt, gelu_pre=pre, drop_p=0.1, seed=80),)
             return kk.linear_dx_gelu(x, wt, pre, 0.1 if case == "gelu_bwd" else 0.0, 79)
         if case in ("gelu_aux", "gelu_aux_k384"):   # fc1: GELU + the pre-activation side output
             drop = 0.1 if case == "gelu_aux" else 0.0
