@@ -85,3 +85,25 @@ def test_binding_argument_counts_match_header():
     for name, (_, argtypes) in _lib._SIGS.items():
         assert name in decls, name
         assert len(argtypes) == decls[name], (name, len(argtypes), decls[name])
+
+
+def test_gemm_tuning_defaults_match_the_library():
+    """sm_gemm_tuning is host-side (no launch): every key kernels.GEMM_TUNING_KEYS names exists
+    in the library, reads back the default kernels.gemm_tuning_nondefault compares against,
+    and a set / reset round trip restores it; an unknown key is refused (-2)."""
+    from ssl_mae_amd import _lib, build, kernels
+    build.build()
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    fn = lib.sm_gemm_tuning
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+    assert list(kernels._GEMM_TUNING_DEFAULTS) == list(kernels.GEMM_TUNING_KEYS)
+    for key, name in enumerate(kernels.GEMM_TUNING_KEYS):
+        prev = ctypes.c_int(-12345)
+        assert fn(key, 0, 0, ctypes.byref(prev)) == 0
+        assert prev.value == kernels._GEMM_TUNING_DEFAULTS[name], name
+        assert fn(key, 1, 7, ctypes.byref(prev)) == 0
+        assert fn(key, 0, 0, ctypes.byref(prev)) == 0 and prev.value == 7
+        assert fn(key, -1, 0, ctypes.byref(prev)) == 0
+        assert fn(key, 0, 0, ctypes.byref(prev)) == 0 and prev.value == kernels._GEMM_TUNING_DEFAULTS[name]
+    assert fn(len(kernels.GEMM_TUNING_KEYS), 0, 0, ctypes.byref(ctypes.c_int())) == -2
