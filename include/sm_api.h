@@ -51,7 +51,8 @@ int sm_gemm_persistent(int mode);
  * 2 / 3 persistent form's minimum N / maximum K at K > 128, 4 tiles per persistent block
  * (-1 = per-K rule, 0 = fully persistent), 5 / 6 tiles per block at K <= 128 / above,
  * 7 minimum K per block for the v_mfma_f32_16x16x32_bf16 K loop of K-major-A tiles
- * (default 1 << 30 = off: measured neutral).
+ * (default 1 << 30 = off: measured neutral), 8 the 384 x 128 pipelined weight-gradient tile
+ * (gemm_dw384) for outputs it divides (default 1 = on).
  * *prev <- the current value; set > 0 stores value, set < 0 restores the default.
  * Returns 0, or -2 for an unknown key.  Host-side only (no launch). */
 int sm_gemm_tuning(int key, int set, int value, int* prev);

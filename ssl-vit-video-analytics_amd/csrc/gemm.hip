@@ -1127,6 +1127,160 @@ __global__ __launch_bounds__(BMV * 2, (BMV == 256 && IMP != 5 && IMP != 6 && IMP
                                                                            lds + w * 8192);
 }
 
+// ============================================================ weight gradient, 384 x 128, one block per CU
+// gemm_dw384: the split-K weight gradient (A = dy^T and B = x both M/N-major, fp32 slabs or C)
+// on a 384 x 128 tile -- the step's weight-gradient shapes (384 / 1152 / 1536 x 384 / 1536) divide
+// it exactly -- with one 8-wave block per CU (96 x 64 per wave: 3 x 2 v_mfma_f32_32x32x16_bf16
+// blocks, 5 fragment reads per 6 MFMAs against v2's 4 per 4) and a software pipeline inside the
+// block instead of v2's two resident blocks: two LDS stages (2 x 64 KB) and two register
+// staging sets, so the operands of K-step k + 2 load while k computes and k + 1 is written to the
+// other stage, one barrier per K-step.  The A image is three [64][128] sub-images (the v2 loader
+// and swizzle at ROWS = 128).  The per-element K order is v2's: at the same split count the
+// slabs are bit-identical to v2's (profiles/r06zjk_dw384_ab.txt); it takes its own split count
+// (dw384_splits: whole rounds of one block per CU), which made it 1.6-7.7 % faster than v2 on the
+// step's decoder / stage-2 weight gradients.  CSUM: the n0 == 0 blocks also sum their A chunks per
+// row (v2's fused bias gradient).
+constexpr int DW3_BM = 384, DW3_BN = 128, DW3_SUB = 128;
+constexpr int DW3_STAGE = (DW3_BM + DW3_BN) * BKT * 2;   // 64 KB
+template <bool CSUM>
+__global__ __launch_bounds__(512, 1) void gemm_dw384(GemmArgs g) {
+  constexpr int NT = 512;
+  __shared__ __attribute__((aligned(16))) char lds[2 * DW3_STAGE];
+  const int ntn = (g.N + DW3_BN - 1) / DW3_BN;
+  const int ntiles = ntn * ((g.M + DW3_BM - 1) / DW3_BM);
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int idx = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int zs = idx / ntiles, tile = idx - zs * ntiles;
+  const int m0 = (tile / ntn) * DW3_BM, n0 = (tile % ntn) * DW3_BN;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int wm = (w >> 1) * 96, wn = (w & 1) * 64;
+  const __bf16* A = (const __bf16*)g.A;
+  const __bf16* B = (const __bf16*)g.B;
+  const int kb = g.k_begin + zs * g.k_chunk;
+  const int ke = min(g.K, kb + g.k_chunk);
+  const int nk = ke > kb ? (ke - kb + BKT - 1) / BKT : 0;
+
+  // one loader for the three sub-images (same offsets): the launch requires M % 384 == 0 and
+  // N % 128 == 0, so every column of the tile exists; rows past the split's K read zero
+  TileLoader<DW3_SUB, NT, false> tla;
+  TileLoader<DW3_BN, NT, false> tlb;
+  tla.init(g.lda, DW3_SUB);
+  tlb.init(g.ldb, DW3_BN);
+  typedef uint4 SetA[3][TileLoader<DW3_SUB, NT, false>::CH];
+  typedef uint4 SetB[TileLoader<DW3_BN, NT, false>::CH];
+  auto load = [&](int k0, SetA& ra, SetB& rb) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) tla.load(panel_rsrc(A, (int64_t)k0 * g.lda + m0 + DW3_SUB * q), ke - k0, ra[q]);
+    tlb.load(panel_rsrc(B, (int64_t)k0 * g.ldb + n0), ke - k0, rb);
+  };
+  const bool csum = CSUM && g.colsum != nullptr && n0 == 0;
+  float cs[3][8];
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) cs[q][j] = 0.f;
+  auto store = [&](char* st, const SetA& ra, const SetB& rb) {
+    if (csum) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+#pragma unroll
+        for (int i = 0; i < TileLoader<DW3_SUB, NT, false>::CH; ++i) {
+          const bf16x8 v = __builtin_bit_cast(bf16x8, ra[q][i]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) cs[q][j] += (float)v[j];
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) tla.store(st + q * (DW3_SUB * BKT * 2), ra[q]);
+    tlb.store(st + DW3_BM * BKT * 2, rb);
+  };
+  f32x16 acc[3][2];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  auto compute = [&](const char* st) {
+    const char* lb = st + DW3_BM * BKT * 2;
+#pragma unroll
+    for (int s = 0; s < BKT / 16; ++s) {
+      bf16x8 af[3], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int r = wm + 32 * i;   // 32-row blocks never straddle a 128-row sub-image
+        af[i] = lread_frag_r<false, DW3_SUB>(st + (r >> 7) * (DW3_SUB * BKT * 2), r & (DW3_SUB - 1), s);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfr[j] = lread_frag_r<false, DW3_BN>(lb, wn + 32 * j, s);
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    }
+  };
+  char* L0 = lds;
+  char* L1 = lds + DW3_STAGE;
+  SetA ra0, ra1;
+  SetB rb0, rb1;
+  if (nk > 0) load(kb, ra0, rb0);
+  if (nk > 1) load(kb + BKT, ra1, rb1);
+  if (nk > 0) store(L0, ra0, rb0);
+  __syncthreads();
+  for (int k = 0; k < nk; k += 2) {
+    // even half: K-step k from L0; k + 2 loads into set 0; k + 1 (set 1) goes to L1
+    if (k + 2 < nk) load(kb + (k + 2) * BKT, ra0, rb0);
+    compute(L0);
+    if (k + 1 < nk) store(L1, ra1, rb1);
+    __syncthreads();
+    if (k + 1 >= nk) break;
+    // odd half: K-step k + 1 from L1; k + 3 loads into set 1; k + 2 (set 0) goes to L0
+    if (k + 3 < nk) load(kb + (k + 3) * BKT, ra1, rb1);
+    compute(L1);
+    if (k + 2 < nk) store(L0, ra0, rb0);
+    __syncthreads();
+  }
+  if (csum) {   // block-uniform: the 32 threads of each sub-image's 8-row chunk group
+    float* red = (float*)lds;   // [512][24]
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[threadIdx.x * 24 + q * 8 + j] = cs[q][j];
+    __syncthreads();
+    if ((int)threadIdx.x < DW3_BM) {
+      const int c = threadIdx.x, q = c >> 7, cc = c & 127, cg = cc >> 3, j = cc & 7;
+      float sum = 0.f;
+      for (int u = 0; u < NT / 16; ++u) sum += red[(u * 16 + cg) * 24 + q * 8 + j];
+      if (m0 + c < g.M) g.colsum[(int64_t)zs * g.M + m0 + c] = sum;
+    }
+    __syncthreads();
+  }
+  // split-K slab of this z: raw fp32 runs (gemm_epilogue's partial path; splits > 1 only)
+  const int h = l >> 5;
+  float* slab = g.partial + (int64_t)zs * g.M * g.N;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int64_t row = m0 + wm + 32 * i + (l & 31);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[i][j][8 * p + e]),
+                                                           __float_as_uint(acc[i][j][8 * p + 4 + e]), false, false);
+          v[e] = __uint_as_float(sw[0]);
+          v[4 + e] = __uint_as_float(sw[1]);
+        }
+        const int col = n0 + wn + 32 * j + 16 * p + 8 * h;
+        if (row < g.M && col < g.N) store8(slab + row * g.N + col, v);
+      }
+  }
+}
+
 // ============================================================ bf16 GEMM, persistent + pipelined
 // gemm_bf16_pp: v2's tile (256 x 128 x 64 on 8 waves of 64 x 64, the same operand images,
 // fragment reads, MFMA order and elementwise epilogue: outputs bit-identical to v2) in
@@ -1804,10 +1958,10 @@ int choose_splits(int M, int N, int K, bool bf16) {
 // Tuning knobs (A/B measurement runs only; scripts/ set them through sm_gemm_tuning, the
 // product path never changes them).  Defaults are the measured best per shape family.
 enum { TUNE_VARIANT = 0, TUNE_PP = 1, TUNE_PP_MINN = 2, TUNE_PP_MAXK = 3, TUNE_PP_ROUNDS = 4,
-       TUNE_PP_ROUNDS_SMALLK = 5, TUNE_PP_ROUNDS_MIDK = 6, TUNE_MF16_MINK = 7, TUNE_COUNT = 8 };
+       TUNE_PP_ROUNDS_SMALLK = 5, TUNE_PP_ROUNDS_MIDK = 6, TUNE_MF16_MINK = 7, TUNE_DW384 = 8, TUNE_COUNT = 9 };
 constexpr int kMF16Off = 1 << 30;
-constexpr int kTuneDefault[TUNE_COUNT] = {0, 1, 128, 6 * BKT, -1, 8, 2, kMF16Off};
-int g_tune[TUNE_COUNT] = {0, 1, 128, 6 * BKT, -1, 8, 2, kMF16Off};
+constexpr int kTuneDefault[TUNE_COUNT] = {0, 1, 128, 6 * BKT, -1, 8, 2, kMF16Off, 1};
+int g_tune[TUNE_COUNT] = {0, 1, 128, 6 * BKT, -1, 8, 2, kMF16Off, 1};
 int gemm_variant(int M, int N, int K) {
   const int forced = (g_tune[TUNE_VARIANT] >= 1 && g_tune[TUNE_VARIANT] <= 3) ? g_tune[TUNE_VARIANT] : 0;
   if (forced) return forced;
@@ -1890,8 +2044,36 @@ bool launch_pp(const GemmArgs& g, hipStream_t st) {
   return true;
 }
 
+// split count for gemm_dw384 (one block per CU): the largest R <= 2 whole rounds of the CUs that
+// stays within the v2 split count the caller's workspace was sized for
+int dw384_splits(int M, int N, int s_v2) {
+  if (!g_tune[TUNE_DW384] || M % DW3_BM || N % DW3_BN || s_v2 <= 1) return s_v2;
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) {
+      (void)hipGetLastError();
+      cus = 256;
+    }
+  }
+  const int tiles = (M / DW3_BM) * (N / DW3_BN);
+  for (int r = 2; r >= 1; --r) {
+    const int sr = r * cus / tiles;
+    if (sr >= 2 && sr <= s_v2) return sr;
+  }
+  return s_v2;
+}
 template <bool AK, bool BK, typename TC, bool VEC>
 void launch_bf16(const GemmArgs& g, int splits, hipStream_t st) {
+  if constexpr (!AK && !BK && sizeof(TC) == 4 && VEC) {
+    // weight gradients on the 384 x 128 pipelined tile (gemm_dw384) where it divides the output
+    if (g_tune[TUNE_DW384] && g.M % DW3_BM == 0 && g.N % DW3_BN == 0 && g.partial != nullptr) {
+      const int t384 = (g.N / DW3_BN) * (g.M / DW3_BM);
+      if (g.colsum) hipLaunchKernelGGL((gemm_dw384<true>), dim3(t384 * splits), dim3(512), 0, st, g);
+      else hipLaunchKernelGGL((gemm_dw384<false>), dim3(t384 * splits), dim3(512), 0, st, g);
+      return;
+    }
+  }
   const int v = gemm_variant(g.M, g.N, g.K);
   const int bm = variant_bm(v), bn = variant_bn(v);
   const int tiles = ((g.N + bn - 1) / bn) * ((g.M + bm - 1) / bm);
@@ -2069,6 +2251,7 @@ static int gemm_run(int ab_dtype, int c_dtype, int a_layout, int b_layout, int M
   g.drop_p = drop_p; g.seed = seed; g.row_scale = row_scale; g.rows_per_group = rows_per_group > 0 ? rows_per_group : 1;
   g.colsum = colsum;
   int splits = choose_splits(M, N, K, ab_dtype == SM_BF16);
+  if (ab_dtype == SM_BF16 && c_dtype == SM_F32 && a_layout == 1 && b_layout == 1) splits = dw384_splits(M, N, splits);
   if (splits > 1 && (workspace == nullptr || ws_bytes < (int64_t)splits * M * N * 4)) splits = 1;
   const int bk = ab_dtype == SM_BF16 ? BKT : FBK;
   if (K <= 0) {  // empty reduction: C = beta*C + bias (epilogue only)
@@ -2469,7 +2652,7 @@ extern "C" int sm_linear_dw_bias(int rows, int nout, int nin, const void* dy, co
     // dW^T[nin][nout] = x^T dy (split-K slabs), reduced into dW[nout][nin] through the
     // transposed store; db = column sums of dy by the colsum kernel (the fused row sums
     // follow the A operand, which is x here)
-    const int s = choose_splits(nin, nout, rows, true);
+    const int s = dw384_splits(nin, nout, choose_splits(nin, nout, rows, true));
     const int64_t gbytes = (int64_t)s * nout * nin * 4;
     GemmArgs g{};
     g.M = nin; g.N = nout; g.K = rows; g.A = x; g.lda = nin; g.B = dy; g.ldb = nout; g.C = dW; g.ldc = nin;
