@@ -52,7 +52,8 @@ int sm_gemm_persistent(int mode);
  * (-1 = per-K rule, 0 = fully persistent), 5 / 6 tiles per block at K <= 128 / above,
  * 7 minimum K per block for the v_mfma_f32_16x16x32_bf16 K loop of K-major-A tiles
  * (default 1 << 30 = off: measured neutral), 8 the 384 x 128 pipelined weight-gradient tile
- * (gemm_dw384) for outputs it divides (default 1 = on).
+ * (gemm_dw384) for outputs it divides (default 1 = on), 9 keep such outputs untransposed in
+ * sm_linear_dw_bias (fused bias gradient; default 1).
  * *prev <- the current value; set > 0 stores value, set < 0 restores the default.
  * Returns 0, or -2 for an unknown key.  Host-side only (no launch). */
 int sm_gemm_tuning(int key, int set, int value, int* prev);

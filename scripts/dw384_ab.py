@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--key", default="dw384", help="the 0 / 1 tuning key to A/B (dw384, dw384_notr)")
     a = ap.parse_args()
     B = a.batch
     dev = "cuda"
@@ -34,14 +35,14 @@ def main():
         times = {0: [], 1: []}
         for _ in range(a.rounds):
             for arm in (0, 1):
-                prev = K.gemm_tuning("dw384", arm)
+                prev = K.gemm_tuning(a.key, arm)
                 times[arm].append(timeit(lambda: K.linear_dw_bias(dy, x, gw[arm], gb[arm]), a.iters))
-                K.gemm_tuning("dw384", prev)
+                K.gemm_tuning(a.key, prev)
         same = ((gw[0] - gw[1]).abs().max() / gw[0].abs().max()).item()
         med = {k: sorted(v)[len(v) // 2] for k, v in times.items()}
         f = 2.0 * rows * nout * nin
-        print(f"dW {name}: rows={rows} nout={nout} nin={nin}  v2 {med[0]:7.3f} ms ({f / med[0] / 1e9:6.1f} TF/s) | "
-              f"dw384 {med[1]:7.3f} ms ({f / med[1] / 1e9:6.1f} TF/s, {(med[1] / med[0] - 1) * 100:+.1f} %) | "
+        print(f"dW {name}: rows={rows} nout={nout} nin={nin}  {a.key}=0 {med[0]:7.3f} ms ({f / med[0] / 1e9:6.1f} TF/s) | "
+              f"{a.key}=1 {med[1]:7.3f} ms ({f / med[1] / 1e9:6.1f} TF/s, {(med[1] / med[0] - 1) * 100:+.1f} %) | "
               f"dW max rel diff {same:.1e}", flush=True)
         del dy, x
         torch.cuda.empty_cache()

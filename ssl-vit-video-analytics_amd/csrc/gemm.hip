@@ -1958,10 +1958,11 @@ int choose_splits(int M, int N, int K, bool bf16) {
 // Tuning knobs (A/B measurement runs only; scripts/ set them through sm_gemm_tuning, the
 // product path never changes them).  Defaults are the measured best per shape family.
 enum { TUNE_VARIANT = 0, TUNE_PP = 1, TUNE_PP_MINN = 2, TUNE_PP_MAXK = 3, TUNE_PP_ROUNDS = 4,
-       TUNE_PP_ROUNDS_SMALLK = 5, TUNE_PP_ROUNDS_MIDK = 6, TUNE_MF16_MINK = 7, TUNE_DW384 = 8, TUNE_COUNT = 9 };
+       TUNE_PP_ROUNDS_SMALLK = 5, TUNE_PP_ROUNDS_MIDK = 6, TUNE_MF16_MINK = 7, TUNE_DW384 = 8,
+       TUNE_DW384_NOTR = 9, TUNE_COUNT = 10 };
 constexpr int kMF16Off = 1 << 30;
-constexpr int kTuneDefault[TUNE_COUNT] = {0, 1, 128, 6 * BKT, -1, 8, 2, kMF16Off, 1};
-int g_tune[TUNE_COUNT] = {0, 1, 128, 6 * BKT, -1, 8, 2, kMF16Off, 1};
+constexpr int kTuneDefault[TUNE_COUNT] = {0, 1, 128, 6 * BKT, -1, 8, 2, kMF16Off, 1, 1};
+int g_tune[TUNE_COUNT] = {0, 1, 128, 6 * BKT, -1, 8, 2, kMF16Off, 1, 1};
 int gemm_variant(int M, int N, int K) {
   const int forced = (g_tune[TUNE_VARIANT] >= 1 && g_tune[TUNE_VARIANT] <= 3) ? g_tune[TUNE_VARIANT] : 0;
   if (forced) return forced;
@@ -2352,6 +2353,10 @@ int64_t tiled_area(int M, int N) {
 // Only when the transposed tiling is exact: [576][192] tiles smaller transposed (192 rows on
 // a 256-row tile) yet ran 3.45 -> 4.40 ms (profiles/r03g_dw_ab.txt).
 bool dw_transposed(int rows, int nout, int nin) {
+  // the 384 x 128 weight-gradient tile divides [384 k][128 n] outputs as they are (fc2's [384][1536]):
+  // no transposed store, and the bias gradient stays fused (no separate column-sum pass): -3.9 %
+  // (profiles/r06zjk_dw384_ab.txt, r06zm)
+  if (g_tune[TUNE_DW384] && g_tune[TUNE_DW384_NOTR] && nout % DW3_BM == 0 && nin % DW3_BN == 0) return false;
   return tiled_area(nin, nout) == (int64_t)nin * nout && tiled_area(nout, nin) * 10 > (int64_t)nout * nin * 11 &&
          choose_splits(nin, nout, rows, true) > 1;
 }

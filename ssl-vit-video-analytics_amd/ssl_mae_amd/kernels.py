@@ -46,7 +46,7 @@ def gemm_persistent(mode=-1):
 
 
 GEMM_TUNING_KEYS = ("variant", "pp", "pp_min_n", "pp_max_k", "pp_rounds", "pp_rounds_small_k", "pp_rounds_mid_k",
-                    "mf16_min_k", "dw384")
+                    "mf16_min_k", "dw384", "dw384_notr")
 
 
 def gemm_tuning(key, value=None, reset=False):
@@ -63,7 +63,7 @@ def gemm_tuning(key, value=None, reset=False):
 
 _GEMM_TUNING_DEFAULTS = {"variant": 0, "pp": 1, "pp_min_n": 128, "pp_max_k": 384, "pp_rounds": -1,
                          "pp_rounds_small_k": 8, "pp_rounds_mid_k": 2, "mf16_min_k": 1 << 30,
-                         "dw384": 1}
+                         "dw384": 1, "dw384_notr": 1}
 
 
 def gemm_tuning_nondefault():

@@ -48,22 +48,28 @@ def rel(a, b):
     return ((a - b).abs().max() / (b.abs().max() + 1e-12)).item()
 
 
-@pytest.mark.parametrize("rows,nout,nin", [(100000, 1536, 384), (100003, 384, 1536), (65536, 1152, 384),
-                                           (99999, 384, 384)])
+@pytest.mark.parametrize("rows,nout,nin,notr", [(100000, 1536, 384, 0), (100003, 384, 1536, 0), (100003, 384, 1536, 1),
+                                                (65536, 1152, 384, 0), (99999, 384, 384, 0)])
 @pytest.mark.parametrize("acc", [False, True])
-def test_dw384_vs_v2(rows, nout, nin, acc):
+def test_dw384_vs_v2(rows, nout, nin, notr, acc):
+    """notr = 1: fc2's [384][1536] gradient kept untransposed on the new tile (fused bias gradient)
+    instead of the transposed form with its separate column sums."""
     kk = KK()
+    prev_notr = kk.gemm_tuning("dw384_notr", notr)
     g = torch.Generator(device=DEV).manual_seed(rows + nout + nin)
     dy = (torch.randn(rows, nout, generator=g, device=DEV) * 0.1).to(torch.bfloat16)
     x = torch.randn(rows, nin, generator=g, device=DEV).to(torch.bfloat16)
     base_w = torch.randn(nout, nin, generator=g, device=DEV) if acc else torch.zeros(nout, nin, device=DEV)
     base_b = torch.randn(nout, generator=g, device=DEV) if acc else torch.zeros(nout, device=DEV)
     out = {}
-    for on in (False, True):
-        gw, gb = base_w.clone(), base_b.clone()
-        with dw384(on):
-            kk.linear_dw_bias(dy, x, gw, gb)
-        out[on] = (gw, gb)
+    try:
+        for on in (False, True):
+            gw, gb = base_w.clone(), base_b.clone()
+            with dw384(on):
+                kk.linear_dw_bias(dy, x, gw, gb)
+            out[on] = (gw, gb)
+    finally:
+        kk.gemm_tuning("dw384_notr", prev_notr)
     assert rel(out[True][0], out[False][0]) < 1e-5
     assert rel(out[True][1], out[False][1]) < 1e-5
     ref_w = base_w + dy.float().t() @ x.float()
